@@ -1,0 +1,263 @@
+"""anothertls_amd — MI355X-native TLS 1.3 record-layer AEAD engine (host-side Python mirror).
+
+The product is the C-ABI library ``libatls.so`` (include/atls.h): hand-written gfx950 HIP
+kernels for AES-GCM and ChaCha20-Poly1305 plus a C++ engine. This module binds it with
+ctypes and mirrors the reference's cipher interface (otsmr/AnotherTLS, paths relative to
+anothertls/src):
+
+* ``CipherSuite`` / ``get_cipher()`` / ``get_key_and_iv_len()`` — crypto/ciphersuite.rs:33-87
+* ``Gcm`` / ``Poly1305`` with ``encrypt(key, iv, plaintext, aad) -> (ct, tag)`` and
+  ``decrypt(key, iv, ct, aad, tag) -> pt`` raising ``TlsError`` — the ``Cipher`` trait,
+  crypto/ciphersuite.rs:12-31 (gcm.rs:131-162, poly1305.rs:69-104)
+* ``Engine`` — the batched record API (atls_engine_*, atls_*_batch) used by the record layer
+  and the benchmark.
+
+There is no CPU fallback: importing works without a GPU, but every compute call raises
+``TlsError(INTERNAL_ERROR)`` when no HIP device is usable, and importing fails loudly if the
+library has not been built (``python -m anothertls_amd._build``).
+"""
+import ctypes
+import enum
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libatls.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"anothertls_amd: {LIB_PATH} is missing; build it with `python -m anothertls_amd._build`")
+_lib = ctypes.CDLL(LIB_PATH)
+
+_c = ctypes
+_u8p = _c.POINTER(_c.c_uint8)
+_lib.atls_seal.argtypes = [_c.c_uint16, _c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_size_t, _c.c_void_p,
+                           _c.c_size_t, _c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_void_p]
+_lib.atls_open.argtypes = [_c.c_uint16, _c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_size_t, _c.c_void_p,
+                           _c.c_size_t, _c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_size_t, _c.c_void_p]
+_lib.atls_engine_create.restype = _c.c_void_p
+_lib.atls_engine_create.argtypes = [_c.c_int]
+_lib.atls_engine_destroy.argtypes = [_c.c_void_p]
+_lib.atls_engine_sync.argtypes = [_c.c_void_p]
+_lib.atls_engine_stream.restype = _c.c_void_p
+_lib.atls_engine_stream.argtypes = [_c.c_void_p]
+_lib.atls_set_keys.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32]
+_lib.atls_seal_batch.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                 _c.c_void_p, _c.c_uint32]
+_lib.atls_open_batch.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
+                                 _c.c_void_p, _c.c_void_p, _c.c_uint32]
+_lib.atls_derive_keys.argtypes = [_c.c_void_p, _c.c_uint16, _c.c_void_p, _c.c_size_t, _c.c_uint32, _c.c_void_p]
+_lib.atls_device_arch.restype = _c.c_char_p
+
+
+class TlsError(Exception):
+    """net/alert.rs:18-45 TlsError; ``code`` is the u8 discriminant."""
+
+    OK = 0
+    BAD_RECORD_MAC = 20
+    ILLEGAL_PARAMETER = 47
+    DECRYPT_ERROR = 50
+    DECODE_ERROR = 51
+    INSUFFICIENT_SECURITY = 71
+    INTERNAL_ERROR = 80
+    _names = {20: "BadRecordMac", 47: "IllegalParameter", 50: "DecryptError", 51: "DecodeError",
+              71: "InsufficientSecurity", 80: "InternalError"}
+
+    def __init__(self, code):
+        self.code = int(code)
+        super().__init__(f"TlsError::{self._names.get(self.code, self.code)} ({self.code})")
+
+
+def _check(rc):
+    if rc != 0:
+        raise TlsError(rc)
+
+
+# ---- numpy mirrors of the C structs (include/atls.h) ----------------------------------------
+KEY_DTYPE = np.dtype([("suite", "<u2"), ("key_len", "u1"), ("iv_len", "u1"), ("key", "u1", 32),
+                      ("static_iv", "u1", 12), ("reserved", "u1", 16)])
+REC_DTYPE = np.dtype([("in_off", "<u8"), ("out_off", "<u8"), ("aux_off", "<u8"), ("seq", "<u8"),
+                      ("len", "<u4"), ("key_slot", "<u4"), ("aad_len", "<u2"), ("content_type", "u1"),
+                      ("mode", "u1"), ("iv_len", "u1"), ("reserved", "u1", 3)])
+OPEN_RESULT_DTYPE = np.dtype([("content_len", "<u4"), ("status", "u1"), ("content_type", "u1"),
+                              ("reserved", "u1", 2)])
+assert KEY_DTYPE.itemsize == 64 and REC_DTYPE.itemsize == 48 and OPEN_RESULT_DTYPE.itemsize == 8
+
+MODE_TLS, MODE_RAW = 0, 1
+FLAG_DEVICE_PTRS, FLAG_DEVICE_RECS, FLAG_NO_SYNC = 1, 2, 4
+
+
+class CipherSuite(enum.IntEnum):
+    """crypto/ciphersuite.rs:33-40."""
+
+    TLS_AES_256_GCM_SHA384 = 0x1302
+    TLS_CHACHA20_POLY1305_SHA256 = 0x1303
+    TLS_AES_128_GCM_SHA256 = 0x1301
+    TLS_EMPTY_RENEGOTIATION_INFO_SCSV = 0x00FF
+
+    @classmethod
+    def new(cls, x):  # ciphersuite.rs:43-51
+        try:
+            return cls(x)
+        except ValueError:
+            raise TlsError(TlsError.INSUFFICIENT_SECURITY) from None
+
+    def as_u16(self):
+        return int(self)
+
+    def get_key_and_iv_len(self):  # ciphersuite.rs:69-77
+        return (16, 12) if self == CipherSuite.TLS_AES_128_GCM_SHA256 else (32, 12)
+
+    def get_hash_len(self):  # ciphersuite.rs:60-68 (get_tshash): SHA-384 for 0x1302, else SHA-256
+        if self == CipherSuite.TLS_EMPTY_RENEGOTIATION_INFO_SCSV:
+            raise TlsError(TlsError.INSUFFICIENT_SECURITY)
+        return 48 if self == CipherSuite.TLS_AES_256_GCM_SHA384 else 32
+
+    def get_cipher(self):  # ciphersuite.rs:78-87
+        if self in (CipherSuite.TLS_AES_256_GCM_SHA384, CipherSuite.TLS_AES_128_GCM_SHA256):
+            return Gcm(self)
+        if self == CipherSuite.TLS_CHACHA20_POLY1305_SHA256:
+            return Poly1305()
+        raise TlsError(TlsError.INSUFFICIENT_SECURITY)
+
+
+def _bytes_arg(b):
+    b = bytes(b)
+    return ctypes.create_string_buffer(b, max(len(b), 1)), len(b)
+
+
+class _DeviceCipher:
+    """The Cipher trait over atls_seal / atls_open (GPU; one record per call)."""
+
+    _suite = None
+
+    def get_cipher_suite(self):
+        return self._suite
+
+    def encrypt(self, key, iv, plaintext, additional_data=b""):
+        k, kl = _bytes_arg(key)
+        v, vl = _bytes_arg(iv)
+        a, al = _bytes_arg(additional_data)
+        p, n = _bytes_arg(plaintext)
+        out = ctypes.create_string_buffer(max(n, 1))
+        tag = ctypes.create_string_buffer(16)
+        _check(_lib.atls_seal(int(self._suite), k, kl, v, vl, a, al, p, n, out, tag))
+        return out.raw[:n], tag.raw
+
+    def decrypt(self, key, iv, ciphertext, additional_data, auth_tag):
+        k, kl = _bytes_arg(key)
+        v, vl = _bytes_arg(iv)
+        a, al = _bytes_arg(additional_data)
+        c, n = _bytes_arg(ciphertext)
+        t, tl = _bytes_arg(auth_tag)
+        out = ctypes.create_string_buffer(max(n, 1))
+        _check(_lib.atls_open(int(self._suite), k, kl, v, vl, a, al, c, n, t, tl, out))
+        return out.raw[:n]
+
+
+class Gcm(_DeviceCipher):
+    """crypto/aes/gcm.rs:15-162 — AES-GCM; AES-128/192/256 chosen by key length (gcm.rs:49)."""
+
+    def __init__(self, cs=CipherSuite.TLS_AES_128_GCM_SHA256):
+        self._suite = CipherSuite(cs)
+
+
+class Poly1305(_DeviceCipher):
+    """crypto/chacha20/poly1305.rs:15-104 — ChaCha20-Poly1305 (RFC 8439, with the reference's
+    last-block behaviour when len % 64 == 0)."""
+
+    _suite = CipherSuite.TLS_CHACHA20_POLY1305_SHA256
+
+
+def device_available():
+    """True when the HIP runtime sees a device the engine can open."""
+    e = _lib.atls_engine_create(int(os.environ.get("ATLS_DEVICE", "0")))
+    if not e:
+        return False
+    _lib.atls_engine_destroy(e)
+    return True
+
+
+def make_keys(entries):
+    """entries: iterable of (suite, key_bytes, static_iv_bytes) -> KEY_DTYPE array."""
+    entries = list(entries)
+    arr = np.zeros(len(entries), dtype=KEY_DTYPE)
+    for i, (suite, key, iv) in enumerate(entries):
+        arr[i]["suite"] = int(suite)
+        arr[i]["key_len"] = len(key)
+        arr[i]["iv_len"] = len(iv)
+        arr[i]["key"][: len(key)] = np.frombuffer(bytes(key), np.uint8)
+        arr[i]["static_iv"][: len(iv)] = np.frombuffer(bytes(iv), np.uint8)
+    return arr
+
+
+def _ptr(x):
+    """numpy array -> host pointer; torch tensor (any device) -> data_ptr; int -> as is."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    raise TypeError(type(x))
+
+
+class Engine:
+    """One HIP device: key slots + batched seal/open (include/atls.h engine API)."""
+
+    def __init__(self, device=0):
+        self._e = _lib.atls_engine_create(int(device))
+        if not self._e:
+            raise TlsError(TlsError.INTERNAL_ERROR)
+        self.device = device
+
+    def close(self):
+        if self._e:
+            _lib.atls_engine_destroy(self._e)
+            self._e = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return _lib.atls_engine_stream(self._e)
+
+    def sync(self):
+        _check(_lib.atls_engine_sync(self._e))
+
+    def set_keys(self, keys):
+        keys = np.ascontiguousarray(keys, dtype=KEY_DTYPE)
+        _check(_lib.atls_set_keys(self._e, keys.ctypes.data, len(keys)))
+
+    def derive_keys(self, suite, secrets):
+        """Key::from_hkdf for each traffic secret (bytes-like, n * hash_len) -> KEY_DTYPE array."""
+        hl = CipherSuite(suite).get_hash_len()
+        buf = np.frombuffer(bytes(secrets), np.uint8)
+        n = len(buf) // hl
+        out = np.zeros(n, dtype=KEY_DTYPE)
+        _check(_lib.atls_derive_keys(self._e, int(suite), buf.ctypes.data, hl, n, out.ctypes.data))
+        return out
+
+    def seal_batch(self, recs, inp, aux, out, tags, flags=0, n=None):
+        n = len(recs) if n is None else n
+        _check(_lib.atls_seal_batch(self._e, _ptr(recs), n, _ptr(inp), _ptr(aux), _ptr(out), _ptr(tags), flags))
+
+    def open_batch(self, recs, inp, aux, tags, out, results, flags=0, n=None):
+        n = len(recs) if n is None else n
+        _check(_lib.atls_open_batch(self._e, _ptr(recs), n, _ptr(inp), _ptr(aux), _ptr(tags), _ptr(out),
+                                    _ptr(results), flags))
+
+
+def abi_version():
+    return _lib.atls_abi_version()
+
+
+def library():
+    """The loaded ctypes library (for the ABI tests)."""
+    return _lib

@@ -1,0 +1,43 @@
+"""Build the gfx950 engine library in-tree: anothertls_amd/libatls.so (hipcc, no torch)."""
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libatls.so")
+SOURCES = ["engine.cpp", "keysetup.hip", "gcm.hip", "chacha.hip", "hkdf.hip"]
+ARCH = os.environ.get("ATLS_OFFLOAD_ARCH", "gfx950")
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(HERE, "..", "include", "atls.h")]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(CSRC, "_obj", src + ".o")
+        os.makedirs(os.path.dirname(obj), exist_ok=True)
+        lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
+               "-munsafe-fp-atomics", *lang, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,416 @@
+// ChaCha20-Poly1305 seal/open for TLS records on gfx950.
+//
+// Restates crypto/chacha20/cipher.rs:12-108 and crypto/chacha20/poly1305.rs:19-99 (RFC 8439
+// AEAD) for a batch of records, including the reference's F4 quirk: ChaCha20::encrypt leaves
+// the last 64-byte block unencrypted when len % 64 == 0 (cipher.rs:99-102), and the tag is
+// computed over that output. Record framing as in net/record.rs:162-240.
+//
+// Mapping: a group of G = 16 lanes per record (4 records per wavefront). Slot j of a record
+// is ChaCha20 block counter j: slot 0 = Poly1305 key generation (poly1305.rs:19-22) plus the
+// AAD blocks, slot j >= 1 = bytes [64(j-1), 64j) of the record (counter starts at 1,
+// poly1305.rs:77). Lane l of the group owns slots j = l (mod 16): each step the group reads and
+// writes one contiguous 1 KiB run of the record.
+// Poly1305 (p = 2^130-5, 26-bit limbs, v_mad_u64_u32 products): a slot's four 16-byte pieces
+// (ciphertext, then the length block) are Horner-folded with r; slots of one lane are folded
+// with r^(4G) = r^64; each lane's partial is finally multiplied by r^e (e in 1..65, square-
+// and-multiply over r^(2^b)) and the group sums the partials mod p.
+// Bytes per record (roofline): read L, write L + 16.
+#include "atls_dev.h"
+
+namespace atls {
+
+constexpr int G = 16;           // lanes per record
+constexpr uint32_t M26 = 0x3ffffffu;
+
+struct P130 { uint32_t l[5]; };
+
+__device__ __forceinline__ P130 p_zero() { P130 z; for (int i = 0; i < 5; i++) z.l[i] = 0; return z; }
+
+// h * r mod p, partially reduced (limbs < 2^26 + small). Inputs: limbs < 2^27.
+__device__ __forceinline__ P130 p_mul(const P130& h, const P130& r) {
+  const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
+  const uint64_t h0 = h.l[0], h1 = h.l[1], h2 = h.l[2], h3 = h.l[3], h4 = h.l[4];
+  uint64_t d0 = h0 * r.l[0] + h1 * s4 + h2 * s3 + h3 * s2 + h4 * s1;
+  uint64_t d1 = h0 * r.l[1] + h1 * r.l[0] + h2 * s4 + h3 * s3 + h4 * s2;
+  uint64_t d2 = h0 * r.l[2] + h1 * r.l[1] + h2 * r.l[0] + h3 * s4 + h4 * s3;
+  uint64_t d3 = h0 * r.l[3] + h1 * r.l[2] + h2 * r.l[1] + h3 * r.l[0] + h4 * s4;
+  uint64_t d4 = h0 * r.l[4] + h1 * r.l[3] + h2 * r.l[2] + h3 * r.l[1] + h4 * r.l[0];
+  P130 o;
+  uint64_t c;
+  c = d0 >> 26; o.l[0] = (uint32_t)d0 & M26; d1 += c;
+  c = d1 >> 26; o.l[1] = (uint32_t)d1 & M26; d2 += c;
+  c = d2 >> 26; o.l[2] = (uint32_t)d2 & M26; d3 += c;
+  c = d3 >> 26; o.l[3] = (uint32_t)d3 & M26; d4 += c;
+  c = d4 >> 26; o.l[4] = (uint32_t)d4 & M26;
+  o.l[0] += (uint32_t)c * 5;
+  o.l[1] += o.l[0] >> 26; o.l[0] &= M26;
+  return o;
+}
+
+// Add a full 16-byte block (raw LE words) plus 2^128 (poly1305.rs:39-43).
+__device__ __forceinline__ void p_add_block(P130& h, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+  h.l[0] += w0 & M26;
+  h.l[1] += ((w0 >> 26) | (w1 << 6)) & M26;
+  h.l[2] += ((w1 >> 20) | (w2 << 12)) & M26;
+  h.l[3] += ((w2 >> 14) | (w3 << 18)) & M26;
+  h.l[4] += (w3 >> 8) | (1u << 24);
+}
+
+__device__ __forceinline__ void p_add(P130& a, const P130& b) { for (int i = 0; i < 5; i++) a.l[i] += b.l[i]; }
+
+__device__ __forceinline__ void p_carry(P130& h) {
+  uint32_t c;
+  c = h.l[0] >> 26; h.l[0] &= M26; h.l[1] += c;
+  c = h.l[1] >> 26; h.l[1] &= M26; h.l[2] += c;
+  c = h.l[2] >> 26; h.l[2] &= M26; h.l[3] += c;
+  c = h.l[3] >> 26; h.l[3] &= M26; h.l[4] += c;
+  c = h.l[4] >> 26; h.l[4] &= M26; h.l[0] += c * 5;
+  c = h.l[0] >> 26; h.l[0] &= M26; h.l[1] += c;
+}
+
+// tag = ((h mod p) + s) mod 2^128 as raw words (poly1305.rs:46-50).
+__device__ __forceinline__ void p_finish(P130 h, const uint32_t s[4], uint32_t t[4]) {
+  p_carry(h);
+  p_carry(h);
+  uint32_t g0 = h.l[0] + 5, c = g0 >> 26; g0 &= M26;
+  uint32_t g1 = h.l[1] + c; c = g1 >> 26; g1 &= M26;
+  uint32_t g2 = h.l[2] + c; c = g2 >> 26; g2 &= M26;
+  uint32_t g3 = h.l[3] + c; c = g3 >> 26; g3 &= M26;
+  uint32_t g4 = h.l[4] + c - (1u << 26);
+  uint32_t mask = (g4 >> 31) - 1u;  // all ones if h >= p
+  uint32_t h0 = (h.l[0] & ~mask) | (g0 & mask), h1 = (h.l[1] & ~mask) | (g1 & mask);
+  uint32_t h2 = (h.l[2] & ~mask) | (g2 & mask), h3 = (h.l[3] & ~mask) | (g3 & mask);
+  uint32_t h4 = (h.l[4] & ~mask) | (g4 & mask);
+  uint32_t w0 = h0 | (h1 << 26), w1 = (h1 >> 6) | (h2 << 20), w2 = (h2 >> 12) | (h3 << 14), w3 = (h3 >> 18) | (h4 << 8);
+  uint64_t f = (uint64_t)w0 + s[0]; t[0] = (uint32_t)f;
+  f = (uint64_t)w1 + s[1] + (f >> 32); t[1] = (uint32_t)f;
+  f = (uint64_t)w2 + s[2] + (f >> 32); t[2] = (uint32_t)f;
+  f = (uint64_t)w3 + s[3] + (f >> 32); t[3] = (uint32_t)f;
+}
+
+__device__ __forceinline__ P130 shfl_p(const P130& v, int src) {
+  P130 o;
+  for (int i = 0; i < 5; i++) o.l[i] = __shfl(v.l[i], src, G);
+  return o;
+}
+
+// ---- ChaCha20 block (chacha20/cipher.rs:56-87) ----
+#define QR(a, b, c, d)                      \
+  a += b; d = rotl32(d ^ a, 16);            \
+  c += d; b = rotl32(b ^ c, 12);            \
+  a += b; d = rotl32(d ^ a, 8);             \
+  c += d; b = rotl32(b ^ c, 7);
+
+__device__ __forceinline__ void chacha_block(const uint32_t kw[8], uint32_t ctr, const uint32_t nw[3], uint32_t o[16]) {
+  uint32_t x0 = 0x61707865, x1 = 0x3320646e, x2 = 0x79622d32, x3 = 0x6b206574;
+  uint32_t x4 = kw[0], x5 = kw[1], x6 = kw[2], x7 = kw[3], x8 = kw[4], x9 = kw[5], x10 = kw[6], x11 = kw[7];
+  uint32_t x12 = ctr, x13 = nw[0], x14 = nw[1], x15 = nw[2];
+#pragma unroll 2
+  for (int i = 0; i < 10; i++) {
+    QR(x0, x4, x8, x12) QR(x1, x5, x9, x13) QR(x2, x6, x10, x14) QR(x3, x7, x11, x15)
+    QR(x0, x5, x10, x15) QR(x1, x6, x11, x12) QR(x2, x7, x8, x13) QR(x3, x4, x9, x14)
+  }
+  o[0] = x0 + 0x61707865; o[1] = x1 + 0x3320646e; o[2] = x2 + 0x79622d32; o[3] = x3 + 0x6b206574;
+  o[4] = x4 + kw[0]; o[5] = x5 + kw[1]; o[6] = x6 + kw[2]; o[7] = x7 + kw[3];
+  o[8] = x8 + kw[4]; o[9] = x9 + kw[5]; o[10] = x10 + kw[6]; o[11] = x11 + kw[7];
+  o[12] = x12 + ctr; o[13] = x13 + nw[0]; o[14] = x14 + nw[1]; o[15] = x15 + nw[2];
+}
+#undef QR
+
+struct ChArgs {
+  const KeySched* ks;
+  const atls_rec* recs;
+  uint32_t n;
+  const uint8_t* in;
+  const uint8_t* aux;
+  uint8_t* out;
+  uint8_t* tags_out;
+  const uint8_t* tags_in;
+  atls_open_result* res;
+  uint32_t* err;
+  uint32_t n_slots;
+};
+
+template <bool OPEN>
+__device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl) {
+  const bool tls = d.mode == ATLS_MODE_TLS;
+  const uint32_t len = d.len;
+  const uint32_t n = (tls && !OPEN) ? len + 1 : len;
+  const uint8_t* src = A.in + d.in_off;
+  uint8_t* dst = A.out + d.out_off;
+  const bool src_al = ((reinterpret_cast<uintptr_t>(src)) & 15u) == 0;
+  const bool dst_al = ((reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+
+  uint32_t kw[8];
+  for (int i = 0; i < 8; i++) kw[i] = k->kw[i];
+  uint32_t nw[3];
+  uint32_t aad_len = 5, hdr0 = 0, hdr1 = 0;
+  const uint8_t* aadp = nullptr;
+  if (tls) {
+    nw[0] = k->siv[0];
+    nw[1] = k->siv[1] ^ bswap32((uint32_t)(d.seq >> 32));
+    nw[2] = k->siv[2] ^ bswap32((uint32_t)d.seq);
+    const uint32_t L = n + 16;
+    hdr0 = 0x17u | (0x03u << 8) | (0x03u << 16) | (((L >> 8) & 0xffu) << 24);
+    hdr1 = L & 0xffu;
+  } else {
+    const uint8_t* iv = A.aux + d.aux_off;
+    for (int w = 0; w < 3; w++)
+      nw[w] = (uint32_t)iv[4 * w] | ((uint32_t)iv[4 * w + 1] << 8) | ((uint32_t)iv[4 * w + 2] << 16) |
+              ((uint32_t)iv[4 * w + 3] << 24);
+    aad_len = d.aad_len;
+    aadp = iv + 12;
+  }
+  const uint32_t na = tls ? 1u : (aad_len + 15u) / 16u;
+  const uint32_t nct = (n + 15u) / 16u;         // ciphertext pieces (pad16, poly1305.rs:52-56)
+  const uint32_t jmax = (n + 63u) / 64u;        // data blocks (f32 ceil is exact below 2^24)
+  const uint32_t jL = nct / 4u + 1u;            // slot holding the length piece (c = nct)
+  const uint32_t Q = na + nct + 1u;             // Poly1305 blocks
+  const bool f4 = (n % 64u) == 0u;              // cipher.rs:100-102: last block not XORed
+
+  P130 r = p_zero(), rp[7];  // rp[b] = r^(2^b)
+  uint32_t sk[4] = {0, 0, 0, 0};
+  P130 acc = p_zero(), innerL = p_zero();
+  int64_t lastnz = -1;
+
+  for (uint32_t base = 0; base <= jL; base += G) {
+    const uint32_t j = base + (uint32_t)gl;
+    const bool active = j <= jL;
+    uint32_t ks[16];
+    if (active && j <= jmax) chacha_block(kw, j, nw, ks);
+    if (base == 0) {
+      // Poly1305 one-time key from block 0 (poly1305.rs:19-22), broadcast within the group.
+      uint32_t r0 = __shfl(ks[0], 0, G), r1 = __shfl(ks[1], 0, G), r2 = __shfl(ks[2], 0, G), r3 = __shfl(ks[3], 0, G);
+      sk[0] = __shfl(ks[4], 0, G); sk[1] = __shfl(ks[5], 0, G); sk[2] = __shfl(ks[6], 0, G); sk[3] = __shfl(ks[7], 0, G);
+      r0 &= 0x0fffffffu; r1 &= 0x0ffffffcu; r2 &= 0x0ffffffcu; r3 &= 0x0ffffffcu;  // clamp (:26)
+      r.l[0] = r0 & M26;
+      r.l[1] = ((r0 >> 26) | (r1 << 6)) & M26;
+      r.l[2] = ((r1 >> 20) | (r2 << 12)) & M26;
+      r.l[3] = ((r2 >> 14) | (r3 << 18)) & M26;
+      r.l[4] = r3 >> 8;
+      rp[0] = r;
+#pragma unroll
+      for (int b = 1; b < 7; b++) rp[b] = p_mul(rp[b - 1], rp[b - 1]);
+    }
+    if (!active) continue;
+
+    P130 inner = p_zero();
+    uint32_t cnt = 0;
+    if (j == 0) {  // AAD blocks (get_mac_data: aad || pad16, poly1305.rs:57-59)
+      for (uint32_t i = 0; i < na; i++) {
+        uint32_t B[4] = {0, 0, 0, 0};
+        if (tls) {
+          B[0] = hdr0; B[1] = hdr1;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; q++)
+            if (16 * i + q < aad_len) B[q >> 2] |= (uint32_t)aadp[16 * i + q] << (8 * (q & 3));
+        }
+        inner = p_mul(inner, r);
+        p_add_block(inner, B[0], B[1], B[2], B[3]);
+        cnt++;
+      }
+    } else {
+      uint32_t C[16];
+      if (j <= jmax) {
+        const uint32_t off = 64u * (j - 1);
+        uint32_t P[16];
+        const uint32_t valid = min(64u, n - off);
+        if (off + 64 <= len && src_al) {
+          const uint4* s4 = reinterpret_cast<const uint4*>(src + off);
+#pragma unroll
+          for (int q = 0; q < 4; q++) {
+            const uint4 v = s4[q];
+            P[4 * q] = v.x; P[4 * q + 1] = v.y; P[4 * q + 2] = v.z; P[4 * q + 3] = v.w;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; q++) P[q] = 0;
+#pragma unroll
+          for (int q = 0; q < 64; q++) {  // compile-time byte index: P stays in registers
+            if ((uint32_t)q < valid) {
+              const uint32_t byte = (off + q < len) ? src[off + q] : (uint32_t)d.content_type;  // record.rs:173
+              P[q >> 2] |= byte << (8 * (q & 3));
+            }
+          }
+        }
+        const bool skip_xor = f4 && j == jmax;
+#pragma unroll
+        for (int q = 0; q < 16; q++) C[q] = skip_xor ? P[q] : (P[q] ^ ks[q]);
+        if (valid < 64) {
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+            const int lo = 4 * q;
+            if ((int)valid < lo + 4) C[q] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - (int)valid)));
+          }
+        }
+        if (valid == 64 && dst_al) {
+          uint4* d4 = reinterpret_cast<uint4*>(dst + off);
+#pragma unroll
+          for (int q = 0; q < 4; q++) d4[q] = make_uint4(C[4 * q], C[4 * q + 1], C[4 * q + 2], C[4 * q + 3]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 64; q++)
+            if ((uint32_t)q < valid) dst[off + q] = (uint8_t)(C[q >> 2] >> (8 * (q & 3)));
+        }
+        if (OPEN) {
+          if (tls) {
+            for (int q = 15; q >= 0; q--) {
+              if (C[q]) {
+                const int bi = 4 * q + (31 - __builtin_clz(C[q])) / 8;
+                lastnz = ((int64_t)(off + bi) << 8) | ((C[q] >> (8 * (bi & 3))) & 0xffu);
+                break;
+              }
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 16; q++) C[q] = P[q];  // MAC runs over the received ciphertext
+          if (valid < 64) {
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+              const int lo = 4 * q;
+              if ((int)valid < lo + 4) C[q] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - (int)valid)));
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; q++) C[q] = 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t c = 4u * (j - 1) + u;
+        if (c < nct) {
+          inner = p_mul(inner, r);
+          p_add_block(inner, C[4 * u], C[4 * u + 1], C[4 * u + 2], C[4 * u + 3]);
+          cnt++;
+        } else if (c == nct) {  // le64(aad_len) || le64(ct_len) (poly1305.rs:63-64)
+          inner = p_mul(inner, r);
+          p_add_block(inner, tls ? 5u : aad_len, 0u, n, 0u);
+          cnt++;
+        }
+      }
+    }
+    if (j == jL) {
+      innerL = inner;  // ref = Q-1: contributes inner * r^1
+    } else {
+      acc = p_mul(acc, rp[6]);  // r^(4G) = r^64
+      p_add(acc, inner);
+    }
+    (void)cnt;
+  }
+
+  // Lane partial: acc covers refs up to its last folded slot jf; contribution acc * r^(Q - ref).
+  P130 contrib = p_zero();
+  {
+    const uint32_t l = (uint32_t)gl;
+    if (jL >= 1 && l <= jL - 1) {
+      const uint32_t jf = l + ((jL - 1 - l) / G) * G;
+      const uint32_t ref = (jf == 0) ? na - 1u : na + 4u * jf - 1u;
+      const uint32_t e = Q - ref;  // 1..65
+      P130 pw = p_zero();
+      pw.l[0] = 1;
+#pragma unroll
+      for (int b = 0; b < 7; b++) {
+        P130 t = p_mul(pw, rp[b]);
+        if ((e >> b) & 1u) pw = t;
+      }
+      if (!(jf == 0 && na == 0)) contrib = p_mul(acc, pw);
+    }
+    if (l == jL % G) p_add(contrib, p_mul(innerL, r));
+  }
+  for (int off = G / 2; off >= 1; off >>= 1) {
+    P130 o = p_zero();
+    for (int i = 0; i < 5; i++) o.l[i] = __shfl_xor(contrib.l[i], off, G);
+    p_add(contrib, o);
+  }
+  uint32_t tag[4];
+  p_finish(contrib, sk, tag);
+
+  if (!OPEN) {
+    if (gl == 0) {
+      uint32_t* tg = reinterpret_cast<uint32_t*>(A.tags_out + 16ull * rec_idx);
+      tg[0] = tag[0]; tg[1] = tag[1]; tg[2] = tag[2]; tg[3] = tag[3];
+    }
+  } else {
+    for (int off = G / 2; off >= 1; off >>= 1) {
+      const int64_t o = __shfl_xor(lastnz, off, G);
+      lastnz = o > lastnz ? o : lastnz;
+    }
+    if (gl == 0) {
+      const uint32_t* tg = reinterpret_cast<const uint32_t*>(A.tags_in + 16ull * rec_idx);
+      const bool ok = (tg[0] == tag[0]) & (tg[1] == tag[1]) & (tg[2] == tag[2]) & (tg[3] == tag[3]);
+      atls_open_result rr;
+      rr.reserved[0] = rr.reserved[1] = 0;
+      if (!tls) {
+        rr.status = ok ? ATLS_OK : ATLS_BAD_RECORD_MAC;
+        rr.content_len = len;
+        rr.content_type = 0;
+      } else if (!ok) {
+        rr.status = ATLS_DECRYPT_ERROR;
+        rr.content_len = 0;
+        rr.content_type = 0;
+      } else {
+        const uint32_t ty = lastnz >= 0 ? (uint32_t)(lastnz & 0xff) : 0u;
+        const bool vt = ty == 0 || ty == 20 || ty == 21 || ty == 22 || ty == 23;
+        rr.status = vt ? ATLS_OK : ATLS_DECODE_ERROR;
+        rr.content_len = lastnz >= 0 ? (uint32_t)(lastnz >> 8) : 0u;
+        rr.content_type = vt ? (uint8_t)ty : 0;
+      }
+      A.res[rec_idx] = rr;
+    }
+  }
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(256) void chacha_kernel(ChArgs A) {
+  const int lane = threadIdx.x & 63;
+  const int gl = lane & (G - 1);
+  const uint32_t group = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+  const uint32_t stride = gridDim.x * blockDim.x / G;
+  for (uint32_t r = group; r < A.n; r += stride) {
+    const atls_rec d = A.recs[r];
+    if (d.key_slot >= A.n_slots || d.mode > ATLS_MODE_RAW) {
+      if (gl == 0) {
+        atomicOr(A.err, 1u);
+        if (OPEN) {
+          atls_open_result rr = {0, ATLS_ILLEGAL_PARAMETER, 0, {0, 0}};
+          A.res[r] = rr;
+        }
+      }
+      continue;
+    }
+    const KeySched* k = A.ks + d.key_slot;
+    if (k->suite != kSuiteChacha) continue;  // AES-GCM records: gcm.hip
+    const bool bad = !k->valid || (d.mode == ATLS_MODE_RAW && d.iv_len != 12);
+    if (bad) {
+      if (gl == 0) {
+        atomicOr(A.err, 1u);
+        if (OPEN) {
+          atls_open_result rr = {0, ATLS_ILLEGAL_PARAMETER, 0, {0, 0}};
+          A.res[r] = rr;
+        }
+      }
+      continue;
+    }
+    chacha_record<OPEN>(A, d, k, r, gl);
+  }
+}
+
+}  // namespace atls
+
+extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
+                                  const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
+                                  atls_open_result* res, uint32_t* err, uint32_t n_slots, int grid,
+                                  hipStream_t s) {
+  if (n == 0) return 0;
+  atls::ChArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, err, n_slots};
+  const uint32_t per_block = 256 / atls::G;
+  uint32_t want = (n + per_block - 1) / per_block;
+  uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
+  if (open)
+    hipLaunchKernelGGL(atls::chacha_kernel<true>, dim3(g), dim3(256), 0, s, A);
+  else
+    hipLaunchKernelGGL(atls::chacha_kernel<false>, dim3(g), dim3(256), 0, s, A);
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}

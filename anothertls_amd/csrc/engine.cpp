@@ -1,0 +1,357 @@
+// Host engine + C ABI (include/atls.h). C++ on the HIP runtime; no torch types.
+//
+// The engine owns one HIP device and one stream, the device key-slot table (KeySched, built
+// by the key-setup kernel), the AES T-table, and staging buffers for callers that hand over
+// host memory. Batches are dispatched to the AES-GCM and ChaCha20-Poly1305 kernels; each
+// kernel walks the whole descriptor array and takes the records of its suite, so descriptors
+// may stay device-resident (ATLS_FLAG_DEVICE_RECS) with no host-side partitioning.
+//
+// atls_seal / atls_open are the Cipher-trait drop-ins (crypto/ciphersuite.rs:12-31): one RAW
+// record through a process-default engine, with the same argument meaning and error codes.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/atls.h"
+#include "atls_dev.h"
+
+extern "C" int atls_launch_build_t0(uint32_t* t0, hipStream_t s);
+extern "C" int atls_launch_key_setup(const atls_key* keys, uint32_t n, void* ks, hipStream_t s);
+extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
+                               const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
+                               atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
+                               int grid, hipStream_t s);
+extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
+                                  const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
+                                  atls_open_result* res, uint32_t* err, uint32_t n_slots, int grid,
+                                  hipStream_t s);
+extern "C" int atls_launch_derive(uint16_t suite, const uint8_t* secrets, uint32_t secret_len, uint32_t n,
+                                  atls_key* out, hipStream_t s);
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool reserve(size_t n) {
+    if (n <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 4096);
+    if (hipMalloc(&p, want) != hipSuccess) return false;
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+}  // namespace
+
+struct atls_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int cus = 256;
+  uint32_t n_slots = 0;
+  bool has_aes = false, has_chacha = false;  // suites present in the key table: skip idle kernels
+  DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
+  std::mutex mu;
+};
+
+namespace {
+
+bool set_dev(atls_engine* e) { return hipSetDevice(e->device) == hipSuccess; }
+
+int finish(atls_engine* e, uint32_t flags) {
+  if (flags & ATLS_FLAG_NO_SYNC) return ATLS_OK;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  uint32_t err = 0;
+  if (hipMemcpy(&err, e->err.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  return err ? ATLS_ILLEGAL_PARAMETER : ATLS_OK;
+}
+
+// Largest byte extent touched by the descriptors (host-memory mode only).
+void extents(const atls_rec* recs, uint32_t n, bool open, size_t* in_end, size_t* out_end, size_t* aux_end) {
+  size_t a = 0, b = 0, c = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    const atls_rec& r = recs[i];
+    const size_t outlen = (r.mode == ATLS_MODE_TLS && !open) ? (size_t)r.len + 1 : r.len;
+    a = std::max(a, (size_t)r.in_off + r.len);
+    b = std::max(b, (size_t)r.out_off + outlen);
+    if (r.mode == ATLS_MODE_RAW) c = std::max(c, (size_t)r.aux_off + r.iv_len + r.aad_len);
+  }
+  *in_end = a;
+  *out_end = b;
+  *aux_end = c;
+}
+
+int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
+              void* out, uint8_t* tags_out, const uint8_t* tags_in, atls_open_result* res, uint32_t flags) {
+  if (!e) return ATLS_INTERNAL_ERROR;
+  if (n == 0) return ATLS_OK;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  if (e->n_slots == 0) return ATLS_ILLEGAL_PARAMETER;
+  hipStream_t s = e->stream;
+  const bool dev_ptrs = flags & ATLS_FLAG_DEVICE_PTRS;
+  const bool dev_recs = flags & ATLS_FLAG_DEVICE_RECS;
+  if (!dev_ptrs && dev_recs) return ATLS_ILLEGAL_PARAMETER;  // host buffers need host-visible descriptors
+
+  const atls_rec* d_recs = recs;
+  if (!dev_recs) {
+    for (uint32_t i = 0; i < n; i++)
+      if (recs[i].key_slot >= e->n_slots || recs[i].mode > ATLS_MODE_RAW) return ATLS_ILLEGAL_PARAMETER;
+    if (!e->recs.reserve(sizeof(atls_rec) * (size_t)n)) return ATLS_INTERNAL_ERROR;
+    if (hipMemcpyAsync(e->recs.p, recs, sizeof(atls_rec) * (size_t)n, hipMemcpyHostToDevice, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    d_recs = (const atls_rec*)e->recs.p;
+  }
+  const uint8_t* d_in = (const uint8_t*)in;
+  const uint8_t* d_aux = (const uint8_t*)aux;
+  uint8_t* d_out = (uint8_t*)out;
+  uint8_t* d_tags_out = tags_out;
+  const uint8_t* d_tags_in = tags_in;
+  atls_open_result* d_res = res;
+  size_t in_end = 0, out_end = 0, aux_end = 0;
+  if (!dev_ptrs) {
+    extents(recs, n, open, &in_end, &out_end, &aux_end);
+    if (!e->in.reserve(in_end + 16) || !e->out.reserve(out_end + 16) || !e->aux.reserve(aux_end + 16) ||
+        !e->tags.reserve(16 * (size_t)n) || !e->res.reserve(sizeof(atls_open_result) * (size_t)n))
+      return ATLS_INTERNAL_ERROR;
+    if (in_end && hipMemcpyAsync(e->in.p, in, in_end, hipMemcpyHostToDevice, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+    if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    if (open && hipMemcpyAsync(e->tags.p, tags_in, 16 * (size_t)n, hipMemcpyHostToDevice, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    d_in = (const uint8_t*)e->in.p;
+    d_aux = (const uint8_t*)e->aux.p;
+    d_out = (uint8_t*)e->out.p;
+    d_tags_out = (uint8_t*)e->tags.p;
+    d_tags_in = (const uint8_t*)e->tags.p;
+    d_res = (atls_open_result*)e->res.p;
+  }
+  if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  int rc = 0;
+  if (e->has_aes)
+    rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
+                         (const uint32_t*)e->t0.p, (uint32_t*)e->err.p, e->n_slots, e->cus * 2, s);
+  if (rc) return rc;
+  if (e->has_chacha)
+    rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
+                            (uint32_t*)e->err.p, e->n_slots, e->cus * 8, s);
+  if (rc) return rc;
+  if (!dev_ptrs) {
+    if (out_end && hipMemcpyAsync(out, e->out.p, out_end, hipMemcpyDeviceToHost, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    if (!open && hipMemcpyAsync(tags_out, e->tags.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    if (open && hipMemcpyAsync(res, e->res.p, sizeof(atls_open_result) * (size_t)n, hipMemcpyDeviceToHost, s) !=
+                    hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    return finish(e, flags & ~ATLS_FLAG_NO_SYNC);
+  }
+  return finish(e, flags);
+}
+
+int key_status(const atls_key& k) {
+  if (k.suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) return k.key_len == 32 ? ATLS_OK : ATLS_ILLEGAL_PARAMETER;
+  if (k.suite == ATLS_TLS_AES_128_GCM_SHA256 || k.suite == ATLS_TLS_AES_256_GCM_SHA384)
+    return (k.key_len == 16 || k.key_len == 24 || k.key_len == 32) ? ATLS_OK : ATLS_ILLEGAL_PARAMETER;
+  return ATLS_INSUFFICIENT_SECURITY;
+}
+
+// ---- process-default engine for the Cipher-trait entry points -----------------------------
+std::mutex g_default_mu;
+atls_engine* g_default = nullptr;
+
+atls_engine* default_engine() {
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  if (!g_default) {
+    const char* dv = std::getenv("ATLS_DEVICE");
+    g_default = atls_engine_create(dv ? std::atoi(dv) : 0);
+  }
+  return g_default;
+}
+
+// One Cipher::encrypt / decrypt call as a single RAW record.
+int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
+           const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, const uint8_t* tag_in, size_t tag_len,
+           uint8_t* out, uint8_t* tag_out) {
+  if (suite != ATLS_TLS_AES_128_GCM_SHA256 && suite != ATLS_TLS_AES_256_GCM_SHA384 &&
+      suite != ATLS_TLS_CHACHA20_POLY1305_SHA256)
+    return ATLS_INSUFFICIENT_SECURITY;  // CipherSuite::get_cipher, ciphersuite.rs:78-87
+  if (suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) {
+    if (key_len != 32 || iv_len != 12) return ATLS_ILLEGAL_PARAMETER;  // poly1305.rs:20 unwrap
+  } else if (key_len != 16 && key_len != 24 && key_len != 32) {
+    return ATLS_ILLEGAL_PARAMETER;  // gcm.rs:49 unwrap
+  }
+  if (iv_len > 255 || aad_len > 0xffff || len > 0xffffffffull) return ATLS_ILLEGAL_PARAMETER;
+  if (open && tag_len != 16) return ATLS_BAD_RECORD_MAC;  // `T != auth_tag` with a wrong-length slice
+  atls_engine* e = default_engine();
+  if (!e) return ATLS_INTERNAL_ERROR;
+  atls_key k;
+  std::memset(&k, 0, sizeof k);
+  k.suite = suite;
+  k.key_len = (uint8_t)key_len;
+  k.iv_len = 12;
+  std::memcpy(k.key, key, key_len);
+  // One engine, one slot: serialise single calls (the batch API is the throughput path).
+  static std::mutex single_mu;
+  std::lock_guard<std::mutex> lk(single_mu);
+  int rc = atls_set_keys(e, &k, 1);
+  if (rc) return rc;
+  std::vector<uint8_t> aux(iv_len + aad_len + 1);
+  if (iv_len) std::memcpy(aux.data(), iv, iv_len);
+  if (aad_len) std::memcpy(aux.data() + iv_len, aad, aad_len);
+  atls_rec r;
+  std::memset(&r, 0, sizeof r);
+  r.len = (uint32_t)len;
+  r.mode = ATLS_MODE_RAW;
+  r.iv_len = (uint8_t)iv_len;
+  r.aad_len = (uint16_t)aad_len;
+  std::vector<uint8_t> inb(len + 1), outb(len + 1);
+  if (len) std::memcpy(inb.data(), in, len);
+  if (!open) {
+    uint8_t tg[16];
+    rc = atls_seal_batch(e, &r, 1, inb.data(), aux.data(), outb.data(), tg, 0);
+    if (rc) return rc;
+    if (len) std::memcpy(out, outb.data(), len);
+    std::memcpy(tag_out, tg, 16);
+    return ATLS_OK;
+  }
+  uint8_t tg[16];
+  std::memcpy(tg, tag_in, 16);
+  atls_open_result res;
+  rc = atls_open_batch(e, &r, 1, inb.data(), aux.data(), tg, outb.data(), &res, 0);
+  if (rc) return rc;
+  if (res.status != ATLS_OK) {
+    if (len) std::memset(out, 0, len);  // no unauthenticated plaintext leaves (reference returns Err)
+    return res.status;
+  }
+  if (len) std::memcpy(out, outb.data(), len);
+  return ATLS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int atls_abi_version(void) { return ATLS_ABI_VERSION; }
+const char* atls_device_arch(void) { return "gfx950"; }
+
+atls_engine* atls_engine_create(int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return nullptr;
+  atls_engine* e = new (std::nothrow) atls_engine();
+  if (!e) return nullptr;
+  e->device = device;
+  hipDeviceProp_t prop;
+  if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    return nullptr;
+  }
+  e->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
+      hipStreamSynchronize(e->stream) != hipSuccess) {
+    atls_engine_destroy(e);
+    return nullptr;
+  }
+  return e;
+}
+
+void atls_engine_destroy(atls_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  for (DevBuf* b : {&e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
+                    &e->secrets, &e->dkeys})
+    b->release();
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int atls_engine_sync(atls_engine* e) {
+  if (!e) return ATLS_INTERNAL_ERROR;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  return finish(e, 0);
+}
+
+void* atls_engine_stream(atls_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int atls_set_keys(atls_engine* e, const atls_key* keys, uint32_t n) {
+  if (!e || (!keys && n)) return ATLS_INTERNAL_ERROR;
+  int status = ATLS_OK;
+  for (uint32_t i = 0; i < n && status == ATLS_OK; i++) status = key_status(keys[i]);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  if (!e->ks.reserve(sizeof(atls::KeySched) * (size_t)std::max<uint32_t>(n, 1)) ||
+      !e->keys_stage.reserve(sizeof(atls_key) * (size_t)std::max<uint32_t>(n, 1)))
+    return ATLS_INTERNAL_ERROR;
+  if (n && hipMemcpyAsync(e->keys_stage.p, keys, sizeof(atls_key) * (size_t)n, hipMemcpyHostToDevice, e->stream) !=
+               hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  if (atls_launch_key_setup((const atls_key*)e->keys_stage.p, n, e->ks.p, e->stream)) return ATLS_INTERNAL_ERROR;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  e->n_slots = n;
+  e->has_aes = e->has_chacha = false;
+  for (uint32_t i = 0; i < n; i++) {
+    if (keys[i].suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) e->has_chacha = true;
+    else e->has_aes = true;  // AES-GCM, or an invalid slot the GCM kernel reports
+  }
+  return status;
+}
+
+int atls_seal_batch(atls_engine* e, const atls_rec* recs, uint32_t n, const void* in, const void* aux, void* out,
+                    uint8_t* tags, uint32_t flags) {
+  return run_batch(e, false, recs, n, in, aux, out, tags, nullptr, nullptr, flags);
+}
+
+int atls_open_batch(atls_engine* e, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
+                    const uint8_t* tags, void* out, atls_open_result* results, uint32_t flags) {
+  return run_batch(e, true, recs, n, in, aux, out, nullptr, tags, results, flags);
+}
+
+int atls_seal(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
+              const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, uint8_t* out, uint8_t tag[16]) {
+  return single(false, suite, key, key_len, iv, iv_len, aad, aad_len, in, len, nullptr, 0, out, tag);
+}
+
+int atls_open(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
+              const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, const uint8_t* tag, size_t tag_len,
+              uint8_t* out) {
+  return single(true, suite, key, key_len, iv, iv_len, aad, aad_len, in, len, tag, tag_len, out, nullptr);
+}
+
+int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, size_t secret_len, uint32_t n,
+                     atls_key* out_keys) {
+  if (!e) return ATLS_INTERNAL_ERROR;
+  if (suite != ATLS_TLS_AES_128_GCM_SHA256 && suite != ATLS_TLS_AES_256_GCM_SHA384 &&
+      suite != ATLS_TLS_CHACHA20_POLY1305_SHA256)
+    return ATLS_INSUFFICIENT_SECURITY;
+  const size_t hl = suite == ATLS_TLS_AES_256_GCM_SHA384 ? 48 : 32;  // CipherSuite::get_tshash
+  if (secret_len != hl) return ATLS_ILLEGAL_PARAMETER;
+  if (n == 0) return ATLS_OK;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  if (!e->secrets.reserve(secret_len * n) || !e->dkeys.reserve(sizeof(atls_key) * (size_t)n)) return ATLS_INTERNAL_ERROR;
+  if (hipMemcpyAsync(e->secrets.p, secrets, secret_len * n, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  if (atls_launch_derive(suite, (const uint8_t*)e->secrets.p, (uint32_t)secret_len, n, (atls_key*)e->dkeys.p, e->stream))
+    return ATLS_INTERNAL_ERROR;
+  if (hipMemcpyAsync(out_keys, e->dkeys.p, sizeof(atls_key) * (size_t)n, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  return hipStreamSynchronize(e->stream) == hipSuccess ? ATLS_OK : ATLS_INTERNAL_ERROR;
+}
+
+}  // extern "C"

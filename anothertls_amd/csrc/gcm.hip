@@ -1,0 +1,431 @@
+// AES-GCM seal/open for TLS records on gfx950 — the hot path of BASELINE.json's north star.
+//
+// Restates crypto/aes/gcm.rs:42-157 (Gcm::gcm, Cipher for Gcm) for a whole batch of
+// records, with the record-layer framing of net/record.rs:162-240 done on the device
+// (inner plaintext = content||type, 5-byte AAD header, nonce = static_iv ^ be64(seq)).
+//
+// Mapping: one record per wavefront (4 waves per workgroup, persistent grid-stride over
+// records). The record's GHASH input sequence is AAD blocks, ciphertext blocks, length
+// block; the wave walks "slots" s = 0..m where slot 0 computes E_K(J0) (gcm.rs:76) and
+// slot s >= 1 is GHASH block g = s-1. Lane l owns slots s = l (mod 64), so every 64-slot
+// step loads/stores one contiguous 1 KiB run of the record (coalesced 16 B per lane).
+//   * AES-CTR: T-table AES (one table, replicated 32x so each lane of a 32-lane LDS group
+//     reads its own bank: conflict-free ds_read_b32), counter block J0 + (b+1).
+//   * GHASH: lane-strided Horner with the fixed multiplier H^64, Y <- Y*H^64 ^ B, where the
+//     multiply is 32 lookups in a per-record 4-bit table in LDS (8 KiB per wave, built
+//     from x^(4p)*H^64, p = 0..31). A 4-bit position table (16 entries x 16 B) spans exactly
+//     one 256-B LDS bank row, so ds_read_b128 lookups never bank-conflict.
+//   * Lane combine: lane l's partial covers blocks whose last index leaves H^e
+//     (1 <= e <= 64) to go; Z_l = Y_l * H^e (bit-serial, per-lane e), XOR-reduced over the
+//     wave, tag = E_K(J0) ^ Z.
+// Bytes per record (roofline): read L, write L + 16 (tag) -- see DESIGN.md §Roofline.
+#include "atls_dev.h"
+
+namespace atls {
+
+constexpr int kWaves = 4;
+constexpr int kTabDwords = 256 * 32;  // replicated T0: entry x, bank b at dword x*32 + b
+constexpr int kGhashU4 = 32 * 16;     // per-wave GHASH table: 32 positions x 16 entries (uint4)
+constexpr size_t kLdsBytes = kTabDwords * 4 + kWaves * kGhashU4 * 16;  // 64 KiB
+
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ---- AES (T-table, raw-word state) -------------------------------------------------------
+#define TT(x) T[(x) << 5]
+template <int NR>
+__device__ __forceinline__ void aes_encrypt_tt(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
+                                               const uint32_t* rk, const uint32_t* T) {
+  s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
+#pragma unroll
+  for (int r = 1; r < NR; r++) {
+    uint32_t t0 = TT(s0 & 0xff) ^ rotl32(TT((s1 >> 8) & 0xff), 8) ^ rotl32(TT((s2 >> 16) & 0xff), 16) ^
+                  rotl32(TT(s3 >> 24), 24) ^ rk[4 * r];
+    uint32_t t1 = TT(s1 & 0xff) ^ rotl32(TT((s2 >> 8) & 0xff), 8) ^ rotl32(TT((s3 >> 16) & 0xff), 16) ^
+                  rotl32(TT(s0 >> 24), 24) ^ rk[4 * r + 1];
+    uint32_t t2 = TT(s2 & 0xff) ^ rotl32(TT((s3 >> 8) & 0xff), 8) ^ rotl32(TT((s0 >> 16) & 0xff), 16) ^
+                  rotl32(TT(s1 >> 24), 24) ^ rk[4 * r + 2];
+    uint32_t t3 = TT(s3 & 0xff) ^ rotl32(TT((s0 >> 8) & 0xff), 8) ^ rotl32(TT((s1 >> 16) & 0xff), 16) ^
+                  rotl32(TT(s2 >> 24), 24) ^ rk[4 * r + 3];
+    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+  }
+  // Final round: SubBytes + ShiftRows; S[x] is byte 1 of T0[x].
+  uint32_t o0 = ((TT(s0 & 0xff) >> 8) & 0xffu) | (TT((s1 >> 8) & 0xff) & 0xff00u) |
+                ((TT((s2 >> 16) & 0xff) << 8) & 0xff0000u) | ((TT(s3 >> 24) << 16) & 0xff000000u);
+  uint32_t o1 = ((TT(s1 & 0xff) >> 8) & 0xffu) | (TT((s2 >> 8) & 0xff) & 0xff00u) |
+                ((TT((s3 >> 16) & 0xff) << 8) & 0xff0000u) | ((TT(s0 >> 24) << 16) & 0xff000000u);
+  uint32_t o2 = ((TT(s2 & 0xff) >> 8) & 0xffu) | (TT((s3 >> 8) & 0xff) & 0xff00u) |
+                ((TT((s0 >> 16) & 0xff) << 8) & 0xff0000u) | ((TT(s1 >> 24) << 16) & 0xff000000u);
+  uint32_t o3 = ((TT(s3 & 0xff) >> 8) & 0xffu) | (TT((s0 >> 8) & 0xff) & 0xff00u) |
+                ((TT((s1 >> 16) & 0xff) << 8) & 0xff0000u) | ((TT(s2 >> 24) << 16) & 0xff000000u);
+  s0 = o0 ^ rk[4 * NR]; s1 = o1 ^ rk[4 * NR + 1]; s2 = o2 ^ rk[4 * NR + 2]; s3 = o3 ^ rk[4 * NR + 3];
+}
+#undef TT
+
+// ---- GHASH ---------------------------------------------------------------------------------
+// Build the wave's table: entry [p][n] = (nibble n at position p) * H^64, raw words. Position
+// p = 2*byte + (low nibble ? 1 : 0) covers coefficients x^(4p)..x^(4p+3); n's bit 3 is x^(4p).
+__device__ __forceinline__ void ghash_build_table(uint4* tab, const KeySched* k, int lane) {
+  const int p = lane >> 1, half = lane & 1;
+  uint32_t P0[4], P1[4], P2[4], P3[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) P0[w] = k->p4_be[p][w];
+#pragma unroll
+  for (int w = 0; w < 4; w++) P1[w] = P0[w];
+  gf_mulx_be(P1);
+#pragma unroll
+  for (int w = 0; w < 4; w++) P2[w] = P1[w];
+  gf_mulx_be(P2);
+#pragma unroll
+  for (int w = 0; w < 4; w++) P3[w] = P2[w];
+  gf_mulx_be(P3);
+  uint4 r0 = make_uint4(bswap32(P0[0]), bswap32(P0[1]), bswap32(P0[2]), bswap32(P0[3]));
+  uint4 r1 = make_uint4(bswap32(P1[0]), bswap32(P1[1]), bswap32(P1[2]), bswap32(P1[3]));
+  uint4 r2 = make_uint4(bswap32(P2[0]), bswap32(P2[1]), bswap32(P2[2]), bswap32(P2[3]));
+  uint4 r3 = make_uint4(bswap32(P3[0]), bswap32(P3[1]), bswap32(P3[2]), bswap32(P3[3]));
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int nv = half * 8 + j;
+    uint4 e = make_uint4(0, 0, 0, 0);
+    if (nv & 8) { e.x ^= r0.x; e.y ^= r0.y; e.z ^= r0.z; e.w ^= r0.w; }
+    if (nv & 4) { e.x ^= r1.x; e.y ^= r1.y; e.z ^= r1.z; e.w ^= r1.w; }
+    if (nv & 2) { e.x ^= r2.x; e.y ^= r2.y; e.z ^= r2.z; e.w ^= r2.w; }
+    if (nv & 1) { e.x ^= r3.x; e.y ^= r3.y; e.z ^= r3.z; e.w ^= r3.w; }
+    tab[p * 16 + nv] = e;
+  }
+}
+
+// y <- y * H^64 (raw words) via 32 table lookups.
+__device__ __forceinline__ void ghash_mul_tab(uint32_t& y0, uint32_t& y1, uint32_t& y2, uint32_t& y3,
+                                              const uint4* tab) {
+  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+  const uint32_t y[4] = {y0, y1, y2, y3};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int byte = 4 * i + b;
+      const uint4 eh = tab[(2 * byte) * 16 + ((y[i] >> (8 * b + 4)) & 15u)];
+      const uint4 el = tab[(2 * byte + 1) * 16 + ((y[i] >> (8 * b)) & 15u)];
+      a0 ^= eh.x ^ el.x; a1 ^= eh.y ^ el.y; a2 ^= eh.z ^ el.z; a3 ^= eh.w ^ el.w;
+    }
+  }
+  y0 = a0; y1 = a1; y2 = a2; y3 = a3;
+}
+
+// ---- byte helpers for partial / unaligned blocks -------------------------------------------
+__device__ __forceinline__ void put_byte(uint32_t w[4], int q, uint32_t v) { w[q >> 2] |= v << (8 * (q & 3)); }
+__device__ __forceinline__ uint32_t get_byte(const uint32_t w[4], int q) { return (w[q >> 2] >> (8 * (q & 3))) & 0xffu; }
+
+// Highest non-zero byte index (< valid) of a raw block, or -1.
+__device__ __forceinline__ int last_nonzero(const uint32_t w[4], int valid) {
+  int r = -1;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint32_t x = w[i];
+    const int lo = 4 * i;
+    if (valid < lo + 4) x &= (valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
+    if (x) r = lo + (31 - __builtin_clz(x)) / 8;
+  }
+  return r;
+}
+
+struct GcmArgs {
+  const KeySched* ks;
+  const atls_rec* recs;
+  uint32_t n;
+  const uint8_t* in;
+  const uint8_t* aux;
+  uint8_t* out;
+  uint8_t* tags_out;       // seal
+  const uint8_t* tags_in;  // open
+  atls_open_result* res;   // open
+  const uint32_t* t0;      // 256-entry T-table in global memory
+  uint32_t* err;           // sticky error word
+  uint32_t n_slots;        // key-table size: descriptors are bounds-checked on the device
+};
+
+template <int NR, bool OPEN>
+__device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx,
+                           const uint32_t* T, uint4* gtab, int lane) {
+  uint32_t rk[4 * (NR + 1)];
+#pragma unroll
+  for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = k->rk[i];
+
+  const bool tls = d.mode == ATLS_MODE_TLS;
+  const uint32_t len = d.len;
+  const uint32_t n_aead = (tls && !OPEN) ? len + 1 : len;  // record.rs:172-173 inner plaintext
+  const uint8_t* src = A.in + d.in_off;
+  uint8_t* dst = A.out + d.out_off;
+  const bool src_al = ((reinterpret_cast<uintptr_t>(src)) & 15u) == 0;
+  const bool dst_al = ((reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+
+  // ---- nonce / J0 (gcm.rs:59-74) and AAD ----
+  uint32_t j0[4];  // be words
+  bool is96 = true;
+  uint32_t hdr0 = 0, hdr1 = 0;  // TLS AAD header, raw words
+  const uint8_t* aadp = nullptr;
+  uint32_t aad_len = 5;
+  if (tls) {
+    // key_schedule.rs:51-64: nonce = iv ^ (0^4 || be64(seq)); J0 = nonce || 0x00000001.
+    const uint64_t seq = d.seq;
+    j0[0] = bswap32(k->siv[0]);
+    j0[1] = bswap32(k->siv[1]) ^ (uint32_t)(seq >> 32);
+    j0[2] = bswap32(k->siv[2]) ^ (uint32_t)seq;
+    j0[3] = 1u;
+    const uint32_t L = n_aead + 16;  // record.rs:176-183, truncated to 16 bits
+    hdr0 = 0x17u | (0x03u << 8) | (0x03u << 16) | (((L >> 8) & 0xffu) << 24);
+    hdr1 = L & 0xffu;
+  } else {
+    const uint8_t* iv = A.aux + d.aux_off;
+    const uint32_t iv_len = d.iv_len;
+    aadp = iv + iv_len;
+    aad_len = d.aad_len;
+    if (iv_len == 12) {
+      j0[0] = ((uint32_t)iv[0] << 24) | ((uint32_t)iv[1] << 16) | ((uint32_t)iv[2] << 8) | iv[3];
+      j0[1] = ((uint32_t)iv[4] << 24) | ((uint32_t)iv[5] << 16) | ((uint32_t)iv[6] << 8) | iv[7];
+      j0[2] = ((uint32_t)iv[8] << 24) | ((uint32_t)iv[9] << 16) | ((uint32_t)iv[10] << 8) | iv[11];
+      j0[3] = 1u;
+    } else {
+      // J0 = GHASH_H(IV || 0-pad || [len(IV)]_64), gcm.rs:59-70. Rare (RAW mode only): every
+      // lane computes it redundantly with the bit-serial multiply.
+      is96 = false;
+      uint32_t N[4] = {0, 0, 0, 0};
+      for (uint32_t i = 0; i < iv_len; i += 16) {
+        uint32_t blk[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+          if (i + q < iv_len) blk[q >> 2] |= (uint32_t)iv[i + q] << (24 - 8 * (q & 3));
+        for (int w = 0; w < 4; w++) blk[w] ^= N[w];
+        gf_mul_be(blk, k->h_be, N);
+      }
+      N[3] ^= iv_len * 8u;
+      uint32_t t[4] = {N[0], N[1], N[2], N[3]};
+      gf_mul_be(t, k->h_be, j0);
+    }
+  }
+
+  const uint32_t na = tls ? 1u : (aad_len + 15u) / 16u;
+  const uint32_t nb = (n_aead + 15u) / 16u;
+  const uint32_t m = na + nb + 1u;  // GHASH blocks: AAD, data, length
+  const uint32_t S = m + 1u;        // slots: E(J0) + GHASH blocks
+  const uint32_t in_bytes = len;    // bytes readable from src
+
+  ghash_build_table(gtab, k, lane);
+  wave_lds_sync();
+
+  uint32_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
+  uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0), lane 0
+  int64_t lastnz = -1;                      // OPEN+TLS: (pos << 8 | byte) of last non-zero pt byte
+
+  for (uint32_t base = 0; base < S; base += 64) {
+    const uint32_t s = base + (uint32_t)lane;
+    // ---- counter block J0 + c (gcm.rs:89-96): c = b + 1 for data block b; 0 for slot 0 ----
+    const uint32_t c = (s > na) ? (s - na) : 0u;
+    uint32_t cb[4] = {j0[0], j0[1], j0[2], j0[3]};
+    if (is96) {
+      cb[3] = j0[3] + c;  // (Yi & !0xFFFFFFFF) | counter, counter mod 2^32
+    } else {            // Yi + counter as a 128-bit add
+      uint64_t lo = (((uint64_t)cb[2] << 32) | cb[3]) + c;
+      uint64_t hi = ((uint64_t)cb[0] << 32) | cb[1];
+      if (lo < c) hi++;
+      cb[0] = (uint32_t)(hi >> 32); cb[1] = (uint32_t)hi; cb[2] = (uint32_t)(lo >> 32); cb[3] = (uint32_t)lo;
+    }
+    uint32_t k0 = bswap32(cb[0]), k1 = bswap32(cb[1]), k2 = bswap32(cb[2]), k3 = bswap32(cb[3]);
+    aes_encrypt_tt<NR>(k0, k1, k2, k3, rk, T);
+    if (s == 0) { e0 = k0; e1 = k1; e2 = k2; e3 = k3; }
+    if (s == 0 || s > m) continue;
+
+    const uint32_t g = s - 1;
+    uint32_t B[4] = {0, 0, 0, 0};
+    if (g < na) {  // AAD block (gcm.rs:78-87), zero-padded at the end (bytes.rs:110-121)
+      if (tls) {
+        B[0] = hdr0; B[1] = hdr1;
+      } else {
+        const uint32_t off = g * 16;
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+          if (off + q < aad_len) put_byte(B, q, aadp[off + q]);
+      }
+    } else if (g < na + nb) {  // data block b (gcm.rs:89-119)
+      const uint32_t b = g - na;
+      const uint32_t off = b * 16;
+      uint32_t P[4] = {0, 0, 0, 0};
+      const uint32_t valid = min(16u, n_aead - off);
+      if (off + 16 <= in_bytes && src_al) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src + off);
+        P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; q++) {  // compile-time byte index keeps P in registers
+          if ((uint32_t)q < valid) {
+            uint32_t byte = (off + q < in_bytes) ? src[off + q] : (uint32_t)d.content_type;  // record.rs:173
+            put_byte(P, q, byte);
+          }
+        }
+      }
+      uint32_t C[4] = {P[0] ^ k0, P[1] ^ k1, P[2] ^ k2, P[3] ^ k3};
+      if (valid < 16) {  // (data ^ Ek) >> overflow: only `valid` bytes exist
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+          const int lo = 4 * w;
+          if ((int)valid < lo + 4) C[w] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
+        }
+      }
+      if (valid == 16 && dst_al) {
+        *reinterpret_cast<uint4*>(dst + off) = make_uint4(C[0], C[1], C[2], C[3]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+          if ((uint32_t)q < valid) dst[off + q] = (uint8_t)get_byte(C, q);
+      }
+      if (OPEN) {
+        B[0] = P[0]; B[1] = P[1]; B[2] = P[2]; B[3] = P[3];  // GHASH over the ciphertext input
+        if (tls) {
+          const int j = last_nonzero(C, (int)valid);
+          if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((C[j >> 2] >> (8 * (j & 3))) & 0xffu);
+        }
+      } else {
+        B[0] = C[0]; B[1] = C[1]; B[2] = C[2]; B[3] = C[3];
+      }
+    } else {  // length block: [len(A)]_64 || [len(C)]_64 in bits (gcm.rs:121)
+      const uint64_t abits = (uint64_t)(tls ? 5u : aad_len) * 8u, cbits = (uint64_t)n_aead * 8u;
+      B[0] = bswap32((uint32_t)(abits >> 32)); B[1] = bswap32((uint32_t)abits);
+      B[2] = bswap32((uint32_t)(cbits >> 32)); B[3] = bswap32((uint32_t)cbits);
+    }
+    ghash_mul_tab(y0, y1, y2, y3, gtab);
+    y0 ^= B[0]; y1 ^= B[1]; y2 ^= B[2]; y3 ^= B[3];
+  }
+
+  // ---- lane combine: Z = sum_l Y_l * H^(S - s_last(l)) ----
+  uint32_t z[4] = {0, 0, 0, 0};
+  {
+    const uint32_t l = (uint32_t)lane;
+    int64_t s_last = -1;
+    if (l == 0) { if (m >= 64) s_last = (int64_t)(m / 64) * 64; }
+    else if (l <= m) s_last = (int64_t)l + (int64_t)((m - l) / 64) * 64;
+    if (s_last >= 1) {
+      const uint32_t e = S - (uint32_t)s_last;  // 1..64
+      const uint32_t yb[4] = {bswap32(y0), bswap32(y1), bswap32(y2), bswap32(y3)};
+      uint32_t hp[4];
+#pragma unroll
+      for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e - 1][w];
+      gf_mul_be(yb, hp, z);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int w = 0; w < 4; w++) z[w] ^= __shfl_xor(z[w], off, 64);
+  }
+  const uint32_t t0 = e0 ^ bswap32(z[0]), t1 = e1 ^ bswap32(z[1]), t2 = e2 ^ bswap32(z[2]), t3 = e3 ^ bswap32(z[3]);
+
+  if (!OPEN) {
+    if (lane == 0) {
+      uint32_t* tg = reinterpret_cast<uint32_t*>(A.tags_out + 16ull * rec_idx);
+      tg[0] = t0; tg[1] = t1; tg[2] = t2; tg[3] = t3;
+    }
+  } else {
+    // content-type scan (record.rs:229-237): wave max of (pos << 8 | byte)
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const int64_t o = __shfl_xor(lastnz, off, 64);
+      lastnz = o > lastnz ? o : lastnz;
+    }
+    if (lane == 0) {
+      const uint32_t* tg = reinterpret_cast<const uint32_t*>(A.tags_in + 16ull * rec_idx);
+      const bool ok = (tg[0] == t0) & (tg[1] == t1) & (tg[2] == t2) & (tg[3] == t3);
+      atls_open_result r;
+      r.reserved[0] = r.reserved[1] = 0;
+      if (!tls) {
+        r.status = ok ? ATLS_OK : ATLS_BAD_RECORD_MAC;
+        r.content_len = len;
+        r.content_type = 0;
+      } else if (!ok) {
+        r.status = ATLS_DECRYPT_ERROR;
+        r.content_len = 0;
+        r.content_type = 0;
+      } else {
+        const uint32_t ty = lastnz >= 0 ? (uint32_t)(lastnz & 0xff) : 0u;
+        const bool valid_type = ty == 0 || ty == 20 || ty == 21 || ty == 22 || ty == 23;
+        r.status = valid_type ? ATLS_OK : ATLS_DECODE_ERROR;
+        r.content_len = lastnz >= 0 ? (uint32_t)(lastnz >> 8) : 0u;
+        r.content_type = valid_type ? (uint8_t)ty : 0;
+      }
+      A.res[rec_idx] = r;
+    }
+  }
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(256) void gcm_kernel(GcmArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  for (int i = threadIdx.x; i < kTabDwords; i += blockDim.x) smem[i] = A.t0[i >> 5];
+  __syncthreads();
+  const int wave = (int)uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const uint32_t* T = smem + (lane & 31);
+  uint4* gtab = reinterpret_cast<uint4*>(smem + kTabDwords) + wave * kGhashU4;
+  const uint32_t stride = gridDim.x * kWaves;
+  for (uint32_t r = blockIdx.x * kWaves + wave; r < A.n; r += stride) {
+    atls_rec d = A.recs[r];
+    d.key_slot = uni(d.key_slot);
+    d.len = uni(d.len);
+    d.mode = (uint8_t)uni(d.mode);
+    if (d.key_slot >= A.n_slots || d.mode > ATLS_MODE_RAW) {
+      if (lane == 0) {
+        atomicOr(A.err, 1u);
+        if (OPEN) {
+          atls_open_result rr = {0, ATLS_ILLEGAL_PARAMETER, 0, {0, 0}};
+          A.res[r] = rr;
+        }
+      }
+      continue;
+    }
+    const KeySched* k = A.ks + d.key_slot;
+    const uint32_t suite = uni(k->suite);
+    if (suite == kSuiteChacha) continue;  // ChaCha20-Poly1305 records: chacha.hip
+    if (suite != kSuiteAes128 && suite != kSuiteAes256) {  // CipherSuite::get_cipher fails (:84)
+      if (lane == 0) {
+        atomicOr(A.err, 1u);
+        if (OPEN) {
+          atls_open_result rr = {0, ATLS_INSUFFICIENT_SECURITY, 0, {0, 0}};
+          A.res[r] = rr;
+        }
+      }
+      continue;
+    }
+    const uint32_t nr = uni(k->valid) ? uni(k->nr) : 0u;
+    if (nr == 10) gcm_record<10, OPEN>(A, d, k, r, T, gtab, lane);
+    else if (nr == 14) gcm_record<14, OPEN>(A, d, k, r, T, gtab, lane);
+    else if (nr == 12) gcm_record<12, OPEN>(A, d, k, r, T, gtab, lane);
+    else if (lane == 0) {
+      atomicOr(A.err, 1u);
+      if (OPEN) {
+        atls_open_result rr = {0, ATLS_ILLEGAL_PARAMETER, 0, {0, 0}};
+        A.res[r] = rr;
+      }
+    }
+    wave_lds_sync();  // table reads of this record done before the next record rebuilds it
+  }
+}
+
+}  // namespace atls
+
+extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
+                               const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
+                               atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
+                               int grid, hipStream_t s) {
+  if (n == 0) return 0;
+  atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, err, n_slots};
+  uint32_t want = (n + atls::kWaves - 1) / atls::kWaves;
+  uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
+  if (open)
+    hipLaunchKernelGGL(atls::gcm_kernel<true>, dim3(g), dim3(256), atls::kLdsBytes, s, A);
+  else
+    hipLaunchKernelGGL(atls::gcm_kernel<false>, dim3(g), dim3(256), atls::kLdsBytes, s, A);
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}

@@ -1,0 +1,79 @@
+"""Synthetic TLS record batches (BASELINE.json configs) as engine descriptors.
+
+A batch is: key slots (one per connection, KEY_DTYPE), record descriptors (REC_DTYPE), and
+the byte sizes of the input/output buffers. Payload bytes are generated separately (host
+numpy for tests, device tensors for the benchmark). Records are laid out back to back at
+16-byte aligned offsets; TLS seal output holds content||type ciphertext (len + 1 bytes).
+Connections are assigned round-robin (record i -> slot i % n_keys) and each connection's
+records carry consecutive sequence numbers, as a record layer's writes would.
+"""
+import numpy as np
+
+from . import KEY_DTYPE, MODE_TLS, REC_DTYPE, CipherSuite
+
+SEEDS = {"payload": 0x5EED0001, "keys": 0x5EED0002, "layout": 0x5EED0003}
+
+CONFIGS = {
+    # name: (suite or "mixed", n_records, content_len or (lo, hi)), BASELINE.json configs[1..4]
+    "c2_aes128gcm_64Ki_x_16KiB": (CipherSuite.TLS_AES_128_GCM_SHA256, 65536, 16384),
+    "c3_chacha20poly1305_64Ki_x_1.5KiB": (CipherSuite.TLS_CHACHA20_POLY1305_SHA256, 65536, 1536),
+    "c4_aes256gcm_1Mi_x_16KiB": (CipherSuite.TLS_AES_256_GCM_SHA384, 1048576, 16384),
+    "c5_mixed_256Ki_x_64B-16KiB": ("mixed", 262144, (64, 16384)),
+}
+
+
+def _round16(x):
+    return (x + 15) & ~np.uint64(15) if isinstance(x, np.ndarray) else (x + 15) & ~15
+
+
+def make_keys(n_keys, suites, seed=SEEDS["keys"], key_lens=None):
+    """n_keys slots; suites: array of suite per slot. key_len from the suite unless given."""
+    rng = np.random.default_rng(seed)
+    keys = np.zeros(n_keys, dtype=KEY_DTYPE)
+    keys["suite"] = suites
+    if key_lens is None:
+        key_lens = np.where(np.asarray(suites) == int(CipherSuite.TLS_AES_128_GCM_SHA256), 16, 32)
+    keys["key_len"] = key_lens
+    keys["iv_len"] = 12
+    keys["key"] = rng.integers(0, 256, size=(n_keys, 32), dtype=np.uint8)
+    keys["static_iv"] = rng.integers(0, 256, size=(n_keys, 12), dtype=np.uint8)
+    return keys
+
+
+def tls_batch(n, lens, suites_per_key, n_keys=4096, content_type=23, seq_base=0):
+    """n TLS-mode records; lens: int or array (content lengths); record i uses slot i % n_keys."""
+    n_keys = min(n_keys, n) if n else 1
+    lens = np.broadcast_to(np.asarray(lens, dtype=np.uint64), (n,)).copy()
+    recs = np.zeros(n, dtype=REC_DTYPE)
+    in_sz = _round16(lens)
+    out_sz = _round16(lens + 1)
+    recs["in_off"] = np.concatenate([[0], np.cumsum(in_sz)[:-1]]).astype(np.uint64) if n else []
+    recs["out_off"] = np.concatenate([[0], np.cumsum(out_sz)[:-1]]).astype(np.uint64) if n else []
+    recs["len"] = lens.astype(np.uint32)
+    slots = np.arange(n, dtype=np.uint64) % np.uint64(n_keys)
+    recs["key_slot"] = slots.astype(np.uint32)
+    recs["seq"] = seq_base + np.arange(n, dtype=np.uint64) // np.uint64(n_keys)
+    recs["content_type"] = content_type
+    recs["mode"] = MODE_TLS
+    keys = make_keys(n_keys, suites_per_key(n_keys) if callable(suites_per_key) else
+                     np.full(n_keys, int(suites_per_key), dtype=np.uint16))
+    return dict(keys=keys, recs=recs, in_bytes=int(in_sz.sum()) if n else 0,
+                out_bytes=int(out_sz.sum()) if n else 0, payload=int(lens.sum() + n))
+
+
+def config_batch(name, n=None):
+    """Descriptors for a BASELINE config (optionally the first n records of it)."""
+    suite, n_full, lens = CONFIGS[name]
+    n = n_full if n is None else n
+    if suite == "mixed":
+        rng = np.random.default_rng(SEEDS["layout"])
+        lo, hi = lens
+        L = rng.integers(lo, hi + 1, size=n_full, dtype=np.uint64)[:n]
+
+        def suites(k):
+            r = np.random.default_rng(SEEDS["layout"] + 1)
+            return np.where(r.random(k) < 0.5, int(CipherSuite.TLS_AES_128_GCM_SHA256),
+                            int(CipherSuite.TLS_CHACHA20_POLY1305_SHA256)).astype(np.uint16)
+
+        return tls_batch(n, L, suites)
+    return tls_batch(n, lens, int(suite))

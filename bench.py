@@ -1,0 +1,186 @@
+"""Benchmark: device-resident TLS-record AEAD throughput (BASELINE.json metric) on MI355X.
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2_aes128gcm_64Ki_x_16KiB]
+For N > 1 the driver launches one rank per GPU with torch.distributed.run; each rank seals
+its own pre-sharded, device-resident batch of the config (records are independent, so there
+is no data-path collective: weak scaling). One step = one atls_seal_batch over the whole
+batch. Rank 0 prints one JSON line.
+
+Fields beyond the driver contract:
+  roofline     — dominant kernel (AES-GCM seal): algorithmic bytes per launch (2L+16 per record:
+                 read L, write L ciphertext + 16 tag) / average launch time from HIP events on
+                 the engine's stream; peak 8 TB/s HBM3E; traffic = PMC-measured HBM bytes per
+                 launch from profiles/ (null if not yet profiled).
+  cpu_baseline — the oracle (literal C restatement of the reference's algorithm: byte S-box
+                 AES with bit-serial MixColumns, bit-serial GHASH) on a bounded sample of the
+                 same records, on this host, 1 thread.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "GiB/s device-resident TLS-record AEAD (16 KiB recs); % HBM roofline @1/2/4/8 GPU"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="c2_aes128gcm_64Ki_x_16KiB")
+    p.add_argument("--records", type=int, default=None, help="override records per GPU")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pcie", action="store_true", help="also time host-memory (PCIe-inclusive) batches")
+    return p.parse_args()
+
+
+def cpu_baseline(batch, inbuf_host, budget_s):
+    """Oracle seal of the first records of this rank's batch, 1 thread, until ~budget_s."""
+    import oracle as ora
+
+    keys, recs = batch["keys"], batch["recs"]
+    okeys = (ora.OraKey * len(keys)).from_buffer_copy(keys.tobytes())
+    aux = np.zeros(16, np.uint8)
+    out = np.zeros(int(recs["out_off"][min(len(recs), 4096) - 1]) + 16400, np.uint8)
+    tags = np.zeros(16 * 4096, np.uint8)
+    done, payload, t0 = 0, 0, time.perf_counter()
+    chunk = 4
+    while done < min(len(recs), 4096) and time.perf_counter() - t0 < budget_s:
+        sub = recs[done:done + chunk].copy()
+        orecs = (ora.OraRec * len(sub)).from_buffer_copy(sub.tobytes())
+        ora.seal_batch(okeys, orecs, inbuf_host, aux, out, tags, 1)
+        payload += int(sub["len"].sum()) + len(sub)
+        done += len(sub)
+    dt = time.perf_counter() - t0
+    return dict(value=payload / dt / 2**30, unit="GiB/s", cores=1, kind="port",
+                sample=f"first {done} records of the same batch ({payload} B AEAD payload), oracle/ref_restatement.c "
+                       f"ora_seal_batch, 1 thread, {dt:.1f} s")
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import anothertls_amd as atls
+    from anothertls_amd import workload
+
+    batch = workload.config_batch(args.config, n=args.records)
+    recs = batch["recs"]
+    n = len(recs)
+    eng = atls.Engine(local)
+    eng.set_keys(batch["keys"])
+    g = torch.Generator(device=dev).manual_seed(workload.SEEDS["payload"] + rank)
+    d_in = torch.randint(0, 256, (batch["in_bytes"],), dtype=torch.uint8, device=dev, generator=g)
+    d_out = torch.empty(batch["out_bytes"], dtype=torch.uint8, device=dev)
+    d_tags = torch.empty(16 * n, dtype=torch.uint8, device=dev)
+    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+    d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
+    torch.cuda.synchronize(dev)
+    flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC
+    stream = torch.cuda.ExternalStream(eng.stream, device=dev)
+
+    def step():
+        eng.seal_batch(d_recs.data_ptr(), d_in, d_aux, d_out, d_tags, flags=flags, n=n)
+
+    for _ in range(args.warmup):
+        step()
+    eng.sync()
+
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    eng.sync()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if dist:
+        tdist.barrier()
+    wall = t1 - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    if dist:
+        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
+        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
+        wall = float(tt.item())
+
+    payload = batch["payload"]  # sum of AEAD lengths (content + type byte)
+    value = world * payload * args.steps / wall / 2**30
+    alg_bytes = 2 * payload + 16 * n
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+
+    result = None
+    if rank == 0:
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        if os.path.exists(tf):
+            t = json.load(open(tf)).get(args.config)
+            traffic = t.get("hbm_bytes_per_launch") if t else None
+        suite, _, clen = workload.CONFIGS[args.config]
+        result = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (device torch.randint payload, seeded keys/IVs)",
+            "config": {"workload": args.config, "records_per_gpu": n,
+                       "aead_bytes_per_record": (clen + 1) if isinstance(clen, int) else "content U{64..16384}+1",
+                       "suite": suite if isinstance(suite, str) else suite.name, "key_slots": len(batch["keys"]),
+                       "mode": "TLS (inner type byte, AAD header, per-record nonce derived on device)",
+                       "parallelism": f"records sharded per GPU, dp{world}, no data-path collective"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                         "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            sample = min(n, 4096)
+            h_in = d_in[: int(recs["in_off"][sample - 1]) + int(recs["len"][sample - 1]) + 16].cpu().numpy()
+            result["cpu_baseline"] = cpu_baseline(batch, h_in, args.cpu_seconds)
+        if args.pcie and world == 1:
+            h_in = d_in.cpu().numpy()
+            h_out = np.empty(batch["out_bytes"], np.uint8)
+            h_tags = np.empty(16 * n, np.uint8)
+            eng.seal_batch(recs, h_in, np.zeros(16, np.uint8), h_out, h_tags)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                eng.seal_batch(recs, h_in, np.zeros(16, np.uint8), h_out, h_tags)
+            result["pcie_inclusive_GiBps"] = round(3 * payload / (time.perf_counter() - t0) / 2**30, 3)
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if dist:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+/*
+ * anothertls_amd — MI355X-native TLS 1.3 record-layer AEAD engine. C ABI.
+ *
+ * This is the drop-in boundary for otsmr/AnotherTLS's per-record bulk AEAD path
+ * (paths relative to /root/reference/anothertls/src):
+ *
+ *   trait Cipher { encrypt(&self,key,iv,plaintext,aad) -> Result<(Vec<u8>,[u8;16]),TlsError>;
+ *                  decrypt(&self,key,iv,ciphertext,aad,auth_tag) -> Result<Vec<u8>,TlsError>; }
+ *     crypto/ciphersuite.rs:12-31, produced by CipherSuite::get_cipher() :78-87 and called only from
+ *     RecordPayloadProtection::encrypt / decrypt (net/record.rs:191-193, :217-220).
+ *
+ * atls_seal / atls_open replace Cipher::encrypt / Cipher::decrypt one call at a time.
+ * The engine API (atls_engine_*, atls_*_batch) is the batched form a record layer uses to put
+ * many records (one connection's fragments, or many connections) into one device launch:
+ * TLS mode derives the inner plaintext (content || content_type, record.rs:172-173), the
+ * 5-byte AAD header (record.rs:175-183) and the per-record nonce (key_schedule.rs:51-64)
+ * on the device; RAW mode takes nonce and AAD verbatim (the Cipher trait's contract).
+ *
+ * Rules: plain C types only; caller-owned buffers; nothing unwinds across this boundary;
+ * every entry point returns 0 or a TlsError code (net/alert.rs:18-45). Where the reference
+ * panics (bad key/IV sizes, short fragments) we return ATLS_ILLEGAL_PARAMETER or
+ * ATLS_DECODE_ERROR instead (documented divergence).
+ * All computation runs on the GPU (gfx950); without a usable HIP device every compute
+ * entry point returns ATLS_INTERNAL_ERROR (there is no CPU fallback).
+ */
+#ifndef ANOTHERTLS_AMD_ATLS_H
+#define ANOTHERTLS_AMD_ATLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ATLS_ABI_VERSION 1
+
+/* Status codes = TlsError discriminants, net/alert.rs:18-45. */
+enum {
+  ATLS_OK = 0,
+  ATLS_BAD_RECORD_MAC = 20,       /* tag mismatch in Cipher::decrypt (gcm.rs:150-154, poly1305.rs:93-98) */
+  ATLS_ILLEGAL_PARAMETER = 47,    /* bad key / IV length (reference panics: gcm.rs:49, poly1305.rs:20) */
+  ATLS_DECRYPT_ERROR = 50,        /* record layer's mapping of any cipher error (record.rs:222) */
+  ATLS_DECODE_ERROR = 51,         /* bad inner content type (record.rs:232) / short record */
+  ATLS_INSUFFICIENT_SECURITY = 71,/* unknown suite (ciphersuite.rs:50, :84) */
+  ATLS_INTERNAL_ERROR = 80        /* no device, allocation or launch failure */
+};
+
+/* CipherSuite, crypto/ciphersuite.rs:33-40. 0x1301 and 0x1302 both map to AES-GCM whose key
+ * size (128/192/256) is taken from key_len exactly as Gcm::gcm does (gcm.rs:49). */
+enum {
+  ATLS_TLS_AES_128_GCM_SHA256 = 0x1301,
+  ATLS_TLS_AES_256_GCM_SHA384 = 0x1302,
+  ATLS_TLS_CHACHA20_POLY1305_SHA256 = 0x1303
+};
+
+/* Record modes for the batch API. */
+enum {
+  ATLS_MODE_TLS = 0, /* seal: in = content (len B); AEAD input = content||content_type (len+1 B);
+                        open: in = ciphertext (len B); AAD = [0x17,3,3,(len+16)>>8,(len+16)] for
+                        both; nonce = static_iv ^ be64(seq). Open scans for the content type. */
+  ATLS_MODE_RAW = 1  /* AEAD over len bytes; nonce (iv_len B) then AAD (aad_len B) read from
+                        aux + aux_off; no framing. */
+};
+
+/* Batch flags. */
+enum {
+  ATLS_FLAG_DEVICE_PTRS = 1u, /* in/aux/out/tags/results are device pointers (else host memory,
+                                 staged through pinned buffers with async copies) */
+  ATLS_FLAG_DEVICE_RECS = 2u, /* recs is a device pointer (keeps descriptors resident) */
+  ATLS_FLAG_NO_SYNC = 4u      /* return after enqueueing; call atls_engine_sync() before reading */
+};
+
+/* One connection's write key (a "key slot"). 64 bytes. suite + key + static IV as produced by
+ * Key::from_hkdf (key_schedule.rs:40-50). iv_len must be 12 (key_schedule.rs:44). */
+typedef struct {
+  uint16_t suite;
+  uint8_t key_len;
+  uint8_t iv_len;
+  uint8_t key[32];
+  uint8_t static_iv[12];
+  uint8_t reserved[16];
+} atls_key;
+
+/* One record descriptor. 48 bytes. Offsets are byte offsets into the in/out/aux buffers;
+ * the tag of record i lives at tags + 16*i. out may alias in (in-place). */
+typedef struct {
+  uint64_t in_off;
+  uint64_t out_off;
+  uint64_t aux_off;
+  uint64_t seq; /* TLS mode: per-record sequence number (key_schedule.rs:51-64) */
+  uint32_t len;
+  uint32_t key_slot;
+  uint16_t aad_len;      /* RAW mode */
+  uint8_t content_type;  /* TLS seal: inner content type (record.rs:173) */
+  uint8_t mode;          /* ATLS_MODE_* */
+  uint8_t iv_len;        /* RAW mode nonce length (GCM accepts any length, gcm.rs:59-70) */
+  uint8_t reserved[3];
+} atls_rec;
+
+/* Per-record open result. 8 bytes. */
+typedef struct {
+  uint32_t content_len; /* TLS: bytes before the content-type byte (record.rs:229-237); RAW: len */
+  uint8_t status;       /* ATLS_OK, or TlsError code (TLS: 50 on tag failure, 51 bad type; RAW: 20) */
+  uint8_t content_type; /* TLS: inner content type (0 = RecordType::Invalid, all-zero plaintext) */
+  uint8_t reserved[2];
+} atls_open_result;
+
+typedef struct atls_engine atls_engine;
+
+/* ---- Cipher-trait drop-in (crypto/ciphersuite.rs:12-31) ---------------------------------
+ * atls_seal  <- Cipher::encrypt: out = ciphertext (len B), tag = 16 B.
+ * atls_open  <- Cipher::decrypt: out = plaintext (len B) or ATLS_BAD_RECORD_MAC (a tag of the
+ *               wrong length is a mismatch, as `T != auth_tag` is in the reference).
+ * Host pointers; run on the process-default engine (device 0 or $ATLS_DEVICE). Reentrant. */
+int atls_seal(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
+              const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, uint8_t* out,
+              uint8_t tag[16]);
+int atls_open(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
+              const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, const uint8_t* tag,
+              size_t tag_len, uint8_t* out);
+
+/* ---- Engine ---------------------------------------------------------------------------- */
+atls_engine* atls_engine_create(int device); /* NULL if the device is unusable */
+void atls_engine_destroy(atls_engine* e);
+int atls_engine_sync(atls_engine* e);
+/* HIP stream the engine launches on (hipStream_t as void*), for callers that time or order work. */
+void* atls_engine_stream(atls_engine* e);
+
+/* Install n key slots (host array). Runs the device key-setup kernel: AES round keys, H = E_K(0),
+ * H^1..H^64 and the GHASH table seeds; ChaCha keys are used as given. Replaces previous slots. */
+int atls_set_keys(atls_engine* e, const atls_key* keys, uint32_t n);
+
+/* Seal / open n records. */
+int atls_seal_batch(atls_engine* e, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
+                    void* out, uint8_t* tags, uint32_t flags);
+int atls_open_batch(atls_engine* e, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
+                    const uint8_t* tags, void* out, atls_open_result* results, uint32_t flags);
+
+/* Traffic-key derivation, Key::from_hkdf (key_schedule.rs:40-50): for each of n traffic
+ * secrets (secret_len = 32 for SHA-256 suites, 48 for SHA-384), key = HKDF-Expand-Label(secret,
+ * "key", "", key_len) and iv = HKDF-Expand-Label(secret, "iv", "", 12), written as atls_key
+ * slots (suite, key_len from the suite: 0x1301 -> 16, 0x1302/0x1303 -> 32). Runs on the device. */
+int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, size_t secret_len, uint32_t n,
+                     atls_key* out_keys);
+
+/* Library info: ABI version and the device arch the code objects were built for ("gfx950"). */
+int atls_abi_version(void);
+const char* atls_device_arch(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

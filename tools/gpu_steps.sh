@@ -1,0 +1,28 @@
+#!/bin/bash
+# Run GPU steps on the gpurun box, each under its own time limit. Stops at the first step that
+# faults, aborts or times out (exit codes other than 0/1); test failures (1) do not stop later steps.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+run() {
+  local name=$1 limit=$2; shift 2
+  echo "[$(date +%T)] start $name" >> gpurun_out/steps.log
+  timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" >> gpurun_out/steps.log
+  tail -3 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    pytest_all) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+    bench) run bench 600 python bench.py ;;
+    bench_c3) run bench_c3 600 python bench.py --config c3_chacha20poly1305_64Ki_x_1.5KiB --no-cpu-baseline ;;
+    bench_c5) run bench_c5 600 python bench.py --config c5_mixed_256Ki_x_64B-16KiB --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
