@@ -27,6 +27,16 @@ LIB_PATH = os.path.join(_HERE, "libatls.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"anothertls_amd: {LIB_PATH} is missing; build it with `python -m anothertls_amd._build`")
+
+# One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (same SONAME). If torch is
+# installed, load it first so libatls.so binds to that already-loaded runtime instead of pulling a
+# second copy from /opt/rocm (two runtimes in one process cannot both open the device). torch is
+# used only as plumbing by callers that pass device tensors; the library itself does not need it.
+if os.environ.get("ATLS_NO_TORCH_RUNTIME") != "1":
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 _lib = ctypes.CDLL(LIB_PATH)
 
 _c = ctypes

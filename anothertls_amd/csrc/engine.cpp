@@ -132,6 +132,9 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
       return ATLS_INTERNAL_ERROR;
     if (open && hipMemcpyAsync(e->tags.p, tags_in, 16 * (size_t)n, hipMemcpyHostToDevice, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
+    // Bytes of `out` outside the records must come back unchanged: stage them in too.
+    if (out_end && hipMemcpyAsync(e->out.p, out, out_end, hipMemcpyHostToDevice, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
     d_in = (const uint8_t*)e->in.p;
     d_aux = (const uint8_t*)e->aux.p;
     d_out = (uint8_t*)e->out.p;

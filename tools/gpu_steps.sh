@@ -23,6 +23,10 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     bench_c3) run bench_c3 600 python bench.py --config c3_chacha20poly1305_64Ki_x_1.5KiB --no-cpu-baseline ;;
     bench_c5) run bench_c5 600 python bench.py --config c5_mixed_256Ki_x_64B-16KiB --no-cpu-baseline ;;
+    prof) export TMPDIR=/tmp; run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmc) export TMPDIR=/tmp; run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline && \
+         run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline && \
+         run pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/pmc_sq -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
