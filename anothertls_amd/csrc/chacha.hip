@@ -354,7 +354,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         const uint32_t ty = lastnz >= 0 ? (uint32_t)(lastnz & 0xff) : 0u;
         const bool vt = ty == 0 || ty == 20 || ty == 21 || ty == 22 || ty == 23;
         rr.status = vt ? ATLS_OK : ATLS_DECODE_ERROR;
-        rr.content_len = lastnz >= 0 ? (uint32_t)(lastnz >> 8) : 0u;
+        rr.content_len = (vt && lastnz >= 0) ? (uint32_t)(lastnz >> 8) : 0u;
         rr.content_type = vt ? (uint8_t)ty : 0;
       }
       A.res[rec_idx] = rr;

@@ -353,7 +353,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
         const uint32_t ty = lastnz >= 0 ? (uint32_t)(lastnz & 0xff) : 0u;
         const bool valid_type = ty == 0 || ty == 20 || ty == 21 || ty == 22 || ty == 23;
         r.status = valid_type ? ATLS_OK : ATLS_DECODE_ERROR;
-        r.content_len = lastnz >= 0 ? (uint32_t)(lastnz >> 8) : 0u;
+        r.content_len = (valid_type && lastnz >= 0) ? (uint32_t)(lastnz >> 8) : 0u;
         r.content_type = valid_type ? (uint8_t)ty : 0;
       }
       A.res[rec_idx] = r;

@@ -208,7 +208,10 @@ def test_batch_raw_mode_vs_oracle(eng):
     pt = np.zeros_like(out)
     res = np.zeros(n, atls.OPEN_RESULT_DTYPE)
     eng.open_batch(recs, out, aux, tags, pt, res)
-    assert (res["status"] == 0).all() and np.array_equal(pt[:ioff], inbuf[:ioff])
+    assert (res["status"] == 0).all()
+    for i in range(n):
+        o, L = int(recs[i]["out_off"]), int(recs[i]["len"])
+        assert pt[o:o + L].tobytes() == inbuf[o:o + L].tobytes(), i
 
 
 def test_unaligned_offsets(eng):
@@ -305,13 +308,15 @@ def test_c2_full_size_roundtrip_and_openssl_spotcheck(eng):
     orecs = recs.copy()
     orecs["in_off"] = recs["out_off"]
     orecs["len"] = recs["len"] + 1
-    orecs["out_off"] = recs["in_off"]
-    d_back = torch.zeros_like(d_in)
+    d_back = torch.zeros(batch["out_bytes"], dtype=torch.uint8, device=dev)  # content||type per record
     d_res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
     eng.open_batch(orecs, d_out, d_aux, d_tags, d_back, d_res, flags=atls.FLAG_DEVICE_PTRS)
     res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
     assert (res["status"] == 0).all() and (res["content_len"] == 16384).all()
-    assert torch.equal(d_back, d_in)
+    # size-independent property: open(seal(x)) == x for every record (input stride 16384 B,
+    # output stride 16400 B = round16(content + type byte))
+    back = d_back.view(n, -1)[:, :16384]
+    assert torch.equal(back, d_in.view(n, -1)[:, :16384]) and bool((d_back.view(n, -1)[:, 16384] == 23).all())
     h_in, h_out, h_tags = d_in.cpu().numpy(), d_out.cpu().numpy(), d_tags.cpu().numpy()
     keys = batch["keys"]
     for i in list(range(0, n, 997)) + [n - 1]:
