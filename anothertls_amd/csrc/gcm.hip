@@ -19,14 +19,18 @@
 //     (1 <= e <= 64) to go; Z_l = Y_l * H^e (bit-serial, per-lane e), XOR-reduced over the
 //     wave, tag = E_K(J0) ^ Z.
 // Bytes per record (roofline): read L, write L + 16 (tag) -- see DESIGN.md §Roofline.
+#include <cstdlib>
+
 #include "atls_dev.h"
 
 namespace atls {
 
-constexpr int kWaves = 4;
-constexpr int kTabDwords = 256 * 32;  // replicated T0: entry x, bank b at dword x*32 + b
-constexpr int kGhashU4 = 32 * 16;     // per-wave GHASH table: 32 positions x 16 entries (uint4)
-constexpr size_t kLdsBytes = kTabDwords * 4 + kWaves * kGhashU4 * 16;  // 64 KiB
+constexpr int kNB = 2;                  // independent AES blocks per lane per step (ILP)
+// LDS: [0, 64 KiB) AES tables, row x = 256 B = {T0[x] x32 banks | T1[x] x32 banks}; then one
+// 8 KiB GHASH table per wave. Lane l reads bank (l & 31): conflict-free ds_read_b32.
+constexpr int kTabBytes = 65536;
+constexpr int kGhashBytes = 8192;
+constexpr size_t lds_bytes(int waves) { return kTabBytes + (size_t)waves * kGhashBytes; }
 
 __device__ __forceinline__ void wave_lds_sync() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -34,42 +38,82 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t rot16(uint32_t x) { return (x << 16) | (x >> 16); }
 
-// ---- AES (T-table, raw-word state) -------------------------------------------------------
-#define TT(x) T[(x) << 5]
-template <int NR>
-__device__ __forceinline__ void aes_encrypt_tt(uint32_t& s0, uint32_t& s1, uint32_t& s2, uint32_t& s3,
-                                               const uint32_t* rk, const uint32_t* T) {
-  s0 ^= rk[0]; s1 ^= rk[1]; s2 ^= rk[2]; s3 ^= rk[3];
+__device__ __forceinline__ uint32_t lds_u32(uint32_t byte_addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(byte_addr);
+}
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4u32 lds_u4(uint32_t byte_addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) v4u32*>(byte_addr);
+}
+
+// ---- AES (two-table T-table rounds on raw-word state) -------------------------------------
+// T0[x] = {2S,S,S,3S} (LE), T1 = rotl8(T0). With T2 = rotl16(T0), T3 = rotl16(T1):
+//   col_c = T0[s_c.b0] ^ T1[s_{c+1}.b1] ^ rotl16(T0[s_{c+2}.b2] ^ T1[s_{c+3}.b3] ^ rotl16(rk_c)).
+// Table address of byte k of state word w for this lane's bank: (byte << 8) | lb, one v_perm_b32
+// (selector byte 0 <- lb, byte 1 <- w.byte_k, bytes 2-3 <- 0); lb = 4*(lane & 31); T1 at +128.
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+#define TA(w, sh) perm((w), lb, 0x0c0c0000u | ((4u + (sh) / 8u) << 8))
+template <int NR, int NB>
+__device__ __forceinline__ void aes_encrypt_tt(uint32_t (&s)[NB][4], const uint32_t* rk, const uint32_t* rkr,
+                                               uint32_t lb) {
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) s[b][i] ^= rk[i];
+  }
 #pragma unroll
   for (int r = 1; r < NR; r++) {
-    uint32_t t0 = TT(s0 & 0xff) ^ rotl32(TT((s1 >> 8) & 0xff), 8) ^ rotl32(TT((s2 >> 16) & 0xff), 16) ^
-                  rotl32(TT(s3 >> 24), 24) ^ rk[4 * r];
-    uint32_t t1 = TT(s1 & 0xff) ^ rotl32(TT((s2 >> 8) & 0xff), 8) ^ rotl32(TT((s3 >> 16) & 0xff), 16) ^
-                  rotl32(TT(s0 >> 24), 24) ^ rk[4 * r + 1];
-    uint32_t t2 = TT(s2 & 0xff) ^ rotl32(TT((s3 >> 8) & 0xff), 8) ^ rotl32(TT((s0 >> 16) & 0xff), 16) ^
-                  rotl32(TT(s1 >> 24), 24) ^ rk[4 * r + 2];
-    uint32_t t3 = TT(s3 & 0xff) ^ rotl32(TT((s0 >> 8) & 0xff), 8) ^ rotl32(TT((s1 >> 16) & 0xff), 16) ^
-                  rotl32(TT(s2 >> 24), 24) ^ rk[4 * r + 3];
-    s0 = t0; s1 = t1; s2 = t2; s3 = t3;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const uint32_t s0 = s[b][0], s1 = s[b][1], s2 = s[b][2], s3 = s[b][3];
+      uint32_t t[4];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const uint32_t a = (c == 0 ? s0 : c == 1 ? s1 : c == 2 ? s2 : s3);
+        const uint32_t bb = (c == 0 ? s1 : c == 1 ? s2 : c == 2 ? s3 : s0);
+        const uint32_t cc = (c == 0 ? s2 : c == 1 ? s3 : c == 2 ? s0 : s1);
+        const uint32_t dd = (c == 0 ? s3 : c == 1 ? s0 : c == 2 ? s1 : s2);
+        const uint32_t u = xor3(lds_u32(TA(cc, 16)), lds_u32(TA(dd, 24) + 128), rkr[4 * r + c]);
+        t[c] = xor3(lds_u32(TA(a, 0)), lds_u32(TA(bb, 8) + 128), rot16(u));
+      }
+#pragma unroll
+      for (int c = 0; c < 4; c++) s[b][c] = t[c];
+    }
   }
-  // Final round: SubBytes + ShiftRows; S[x] is byte 1 of T0[x].
-  uint32_t o0 = ((TT(s0 & 0xff) >> 8) & 0xffu) | (TT((s1 >> 8) & 0xff) & 0xff00u) |
-                ((TT((s2 >> 16) & 0xff) << 8) & 0xff0000u) | ((TT(s3 >> 24) << 16) & 0xff000000u);
-  uint32_t o1 = ((TT(s1 & 0xff) >> 8) & 0xffu) | (TT((s2 >> 8) & 0xff) & 0xff00u) |
-                ((TT((s3 >> 16) & 0xff) << 8) & 0xff0000u) | ((TT(s0 >> 24) << 16) & 0xff000000u);
-  uint32_t o2 = ((TT(s2 & 0xff) >> 8) & 0xffu) | (TT((s3 >> 8) & 0xff) & 0xff00u) |
-                ((TT((s0 >> 16) & 0xff) << 8) & 0xff0000u) | ((TT(s1 >> 24) << 16) & 0xff000000u);
-  uint32_t o3 = ((TT(s3 & 0xff) >> 8) & 0xffu) | (TT((s0 >> 8) & 0xff) & 0xff00u) |
-                ((TT((s1 >> 16) & 0xff) << 8) & 0xff0000u) | ((TT(s2 >> 24) << 16) & 0xff000000u);
-  s0 = o0 ^ rk[4 * NR]; s1 = o1 ^ rk[4 * NR + 1]; s2 = o2 ^ rk[4 * NR + 2]; s3 = o3 ^ rk[4 * NR + 3];
+  // Final round (SubBytes, ShiftRows, AddRoundKey): S[x] = byte 1 of T0[x] = byte 2, 3 of T1[x].
+#pragma unroll
+  for (int b = 0; b < NB; b++) {
+    const uint32_t s0 = s[b][0], s1 = s[b][1], s2 = s[b][2], s3 = s[b][3];
+    uint32_t t[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const uint32_t a = (c == 0 ? s0 : c == 1 ? s1 : c == 2 ? s2 : s3);
+      const uint32_t bb = (c == 0 ? s1 : c == 1 ? s2 : c == 2 ? s3 : s0);
+      const uint32_t cc = (c == 0 ? s2 : c == 1 ? s3 : c == 2 ? s0 : s1);
+      const uint32_t dd = (c == 0 ? s3 : c == 1 ? s0 : c == 2 ? s1 : s2);
+      // {T0[a].b1, T0[b].b1} | {T1[c].b2, T1[d].b3}, then ^ rk: two v_perm + one v_bitop3 ((x|y)^z)
+      const uint32_t lo = perm(lds_u32(TA(bb, 8)), lds_u32(TA(a, 0)), 0x0c0c0501u);
+      const uint32_t hi = perm(lds_u32(TA(dd, 24) + 128), lds_u32(TA(cc, 16) + 128), 0x07020c0cu);
+      t[c] = __builtin_amdgcn_bitop3_b32(lo, hi, rk[4 * NR + c], 0x56);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[b][c] = t[c];
+  }
 }
-#undef TT
+#undef TA
 
 // ---- GHASH ---------------------------------------------------------------------------------
-// Build the wave's table: entry [p][n] = (nibble n at position p) * H^64, raw words. Position
-// p = 2*byte + (low nibble ? 1 : 0) covers coefficients x^(4p)..x^(4p+3); n's bit 3 is x^(4p).
-__device__ __forceinline__ void ghash_build_table(uint4* tab, const KeySched* k, int lane) {
+// The wave's table at LDS byte address wb: entry [p][n] = (nibble n at position p) * H^64, raw
+// words, p = 2*byte + (low nibble ? 1 : 0) covering x^(4p)..x^(4p+3) (n's bit 3 is x^(4p)).
+// A position's 16 entries x 16 B fill exactly one 256-B bank row: lookups never conflict.
+__device__ __forceinline__ void ghash_build_table(uint32_t wb, const KeySched* k, int lane) {
   const int p = lane >> 1, half = lane & 1;
   uint32_t P0[4], P1[4], P2[4], P3[4];
 #pragma unroll
@@ -83,38 +127,41 @@ __device__ __forceinline__ void ghash_build_table(uint4* tab, const KeySched* k,
 #pragma unroll
   for (int w = 0; w < 4; w++) P3[w] = P2[w];
   gf_mulx_be(P3);
-  uint4 r0 = make_uint4(bswap32(P0[0]), bswap32(P0[1]), bswap32(P0[2]), bswap32(P0[3]));
-  uint4 r1 = make_uint4(bswap32(P1[0]), bswap32(P1[1]), bswap32(P1[2]), bswap32(P1[3]));
-  uint4 r2 = make_uint4(bswap32(P2[0]), bswap32(P2[1]), bswap32(P2[2]), bswap32(P2[3]));
-  uint4 r3 = make_uint4(bswap32(P3[0]), bswap32(P3[1]), bswap32(P3[2]), bswap32(P3[3]));
+  uint32_t r0[4], r1[4], r2[4], r3[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    r0[w] = bswap32(P0[w]); r1[w] = bswap32(P1[w]); r2[w] = bswap32(P2[w]); r3[w] = bswap32(P3[w]);
+  }
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     const int nv = half * 8 + j;
-    uint4 e = make_uint4(0, 0, 0, 0);
-    if (nv & 8) { e.x ^= r0.x; e.y ^= r0.y; e.z ^= r0.z; e.w ^= r0.w; }
-    if (nv & 4) { e.x ^= r1.x; e.y ^= r1.y; e.z ^= r1.z; e.w ^= r1.w; }
-    if (nv & 2) { e.x ^= r2.x; e.y ^= r2.y; e.z ^= r2.z; e.w ^= r2.w; }
-    if (nv & 1) { e.x ^= r3.x; e.y ^= r3.y; e.z ^= r3.z; e.w ^= r3.w; }
-    tab[p * 16 + nv] = e;
+    uint32_t e[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+      e[w] = ((nv & 8) ? r0[w] : 0u) ^ ((nv & 4) ? r1[w] : 0u) ^ ((nv & 2) ? r2[w] : 0u) ^ ((nv & 1) ? r3[w] : 0u);
+    v4u32 ev = {e[0], e[1], e[2], e[3]};
+    *reinterpret_cast<__attribute__((address_space(3))) v4u32*>(wb + (uint32_t)(p * 256 + nv * 16)) = ev;
   }
 }
 
-// y <- y * H^64 (raw words) via 32 table lookups.
-__device__ __forceinline__ void ghash_mul_tab(uint32_t& y0, uint32_t& y1, uint32_t& y2, uint32_t& y3,
-                                              const uint4* tab) {
+// y <- y * H^64 (raw words) via 32 table lookups. Each nibble's table offset (n * 16) is the
+// nibble's byte of (y & 0xF0F0F0F0) or ((y << 4) & 0xF0F0F0F0), OR-ed onto the wave base.
+__device__ __forceinline__ void ghash_mul_tab(uint32_t (&y)[4], uint32_t wb) {
   uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-  const uint32_t y[4] = {y0, y1, y2, y3};
 #pragma unroll
   for (int i = 0; i < 4; i++) {
+    const uint32_t hi4 = y[i] & 0xF0F0F0F0u, lo4 = (y[i] << 4) & 0xF0F0F0F0u;
 #pragma unroll
     for (int b = 0; b < 4; b++) {
-      const int byte = 4 * i + b;
-      const uint4 eh = tab[(2 * byte) * 16 + ((y[i] >> (8 * b + 4)) & 15u)];
-      const uint4 el = tab[(2 * byte + 1) * 16 + ((y[i] >> (8 * b)) & 15u)];
-      a0 ^= eh.x ^ el.x; a1 ^= eh.y ^ el.y; a2 ^= eh.z ^ el.z; a3 ^= eh.w ^ el.w;
+      const uint32_t byte = 4 * i + b;
+      // address = wb | (nibble << 4): byte 0 from the nibble's byte, bytes 1-2 from wb (one v_perm)
+      const uint32_t sel = 0x0c020100u | (4u + b);
+      const v4u32 eh = lds_u4(perm(hi4, wb, sel) + (2 * byte) * 256);
+      const v4u32 el = lds_u4(perm(lo4, wb, sel) + (2 * byte + 1) * 256);
+      a0 = xor3(a0, eh.x, el.x); a1 = xor3(a1, eh.y, el.y); a2 = xor3(a2, eh.z, el.z); a3 = xor3(a3, eh.w, el.w);
     }
   }
-  y0 = a0; y1 = a1; y2 = a2; y3 = a3;
+  y[0] = a0; y[1] = a1; y[2] = a2; y[3] = a3;
 }
 
 // ---- byte helpers for partial / unaligned blocks -------------------------------------------
@@ -151,10 +198,13 @@ struct GcmArgs {
 
 template <int NR, bool OPEN>
 __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx,
-                           const uint32_t* T, uint4* gtab, int lane) {
-  uint32_t rk[4 * (NR + 1)];
+                           uint32_t lb, uint32_t wb, int lane) {
+  uint32_t rk[4 * (NR + 1)], rkr[4 * (NR + 1)];
 #pragma unroll
-  for (int i = 0; i < 4 * (NR + 1); i++) rk[i] = k->rk[i];
+  for (int i = 0; i < 4 * (NR + 1); i++) {
+    rk[i] = k->rk[i];
+    rkr[i] = rot16(rk[i]);
+  }
 
   const bool tls = d.mode == ATLS_MODE_TLS;
   const uint32_t len = d.len;
@@ -215,90 +265,108 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   const uint32_t S = m + 1u;        // slots: E(J0) + GHASH blocks
   const uint32_t in_bytes = len;    // bytes readable from src
 
-  ghash_build_table(gtab, k, lane);
+  ghash_build_table(wb, k, lane);
   wave_lds_sync();
 
-  uint32_t y0 = 0, y1 = 0, y2 = 0, y3 = 0;
+  uint32_t y[4] = {0, 0, 0, 0};
   uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0), lane 0
   int64_t lastnz = -1;                      // OPEN+TLS: (pos << 8 | byte) of last non-zero pt byte
+  const bool fast_src = src_al, fast_dst = dst_al;
 
-  for (uint32_t base = 0; base < S; base += 64) {
-    const uint32_t s = base + (uint32_t)lane;
-    // ---- counter block J0 + c (gcm.rs:89-96): c = b + 1 for data block b; 0 for slot 0 ----
-    const uint32_t c = (s > na) ? (s - na) : 0u;
-    uint32_t cb[4] = {j0[0], j0[1], j0[2], j0[3]};
-    if (is96) {
-      cb[3] = j0[3] + c;  // (Yi & !0xFFFFFFFF) | counter, counter mod 2^32
-    } else {            // Yi + counter as a 128-bit add
-      uint64_t lo = (((uint64_t)cb[2] << 32) | cb[3]) + c;
-      uint64_t hi = ((uint64_t)cb[0] << 32) | cb[1];
-      if (lo < c) hi++;
-      cb[0] = (uint32_t)(hi >> 32); cb[1] = (uint32_t)hi; cb[2] = (uint32_t)(lo >> 32); cb[3] = (uint32_t)lo;
-    }
-    uint32_t k0 = bswap32(cb[0]), k1 = bswap32(cb[1]), k2 = bswap32(cb[2]), k3 = bswap32(cb[3]);
-    aes_encrypt_tt<NR>(k0, k1, k2, k3, rk, T);
-    if (s == 0) { e0 = k0; e1 = k1; e2 = k2; e3 = k3; }
-    if (s == 0 || s > m) continue;
-
-    const uint32_t g = s - 1;
-    uint32_t B[4] = {0, 0, 0, 0};
-    if (g < na) {  // AAD block (gcm.rs:78-87), zero-padded at the end (bytes.rs:110-121)
-      if (tls) {
-        B[0] = hdr0; B[1] = hdr1;
-      } else {
-        const uint32_t off = g * 16;
+  for (uint32_t base = 0; base < S; base += 64 * kNB) {
+    uint32_t st[kNB][4];
+    uint32_t P[kNB][4];
 #pragma unroll
-        for (int q = 0; q < 16; q++)
-          if (off + q < aad_len) put_byte(B, q, aadp[off + q]);
+    for (int b = 0; b < kNB; b++) {
+      const uint32_t s = base + 64u * b + (uint32_t)lane;
+      // counter block J0 + c (gcm.rs:89-96): c = b + 1 for data block b, 0 for slot 0
+      const uint32_t c = (s > na) ? (s - na) : 0u;
+      uint32_t cb[4] = {j0[0], j0[1], j0[2], j0[3]};
+      if (is96) {
+        cb[3] = j0[3] + c;  // (Yi & !0xFFFFFFFF) | counter, counter mod 2^32
+      } else {            // Yi + counter as a 128-bit add
+        uint64_t lo = (((uint64_t)cb[2] << 32) | cb[3]) + c;
+        uint64_t hi = ((uint64_t)cb[0] << 32) | cb[1];
+        if (lo < c) hi++;
+        cb[0] = (uint32_t)(hi >> 32); cb[1] = (uint32_t)hi; cb[2] = (uint32_t)(lo >> 32); cb[3] = (uint32_t)lo;
       }
-    } else if (g < na + nb) {  // data block b (gcm.rs:89-119)
-      const uint32_t b = g - na;
-      const uint32_t off = b * 16;
-      uint32_t P[4] = {0, 0, 0, 0};
-      const uint32_t valid = min(16u, n_aead - off);
-      if (off + 16 <= in_bytes && src_al) {
-        const uint4 v = *reinterpret_cast<const uint4*>(src + off);
-        P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
-      } else {
 #pragma unroll
-        for (int q = 0; q < 16; q++) {  // compile-time byte index keeps P in registers
-          if ((uint32_t)q < valid) {
-            uint32_t byte = (off + q < in_bytes) ? src[off + q] : (uint32_t)d.content_type;  // record.rs:173
-            put_byte(P, q, byte);
+      for (int w = 0; w < 4; w++) st[b][w] = bswap32(cb[w]);
+      // issue the data load before the AES rounds so HBM latency hides under them
+      P[b][0] = P[b][1] = P[b][2] = P[b][3] = 0;
+      const uint32_t g = s - 1;
+      if (s >= 1 && s <= m && g >= na && g < na + nb) {
+        const uint32_t off = (g - na) * 16;
+        if (off + 16 <= in_bytes && fast_src) {
+          const uint4 v = *reinterpret_cast<const uint4*>(src + off);
+          P[b][0] = v.x; P[b][1] = v.y; P[b][2] = v.z; P[b][3] = v.w;
+        } else {
+          const uint32_t valid = min(16u, n_aead - off);
+#pragma unroll
+          for (int q = 0; q < 16; q++) {  // compile-time byte index keeps P in registers
+            if ((uint32_t)q < valid) {
+              const uint32_t byte = (off + q < in_bytes) ? src[off + q] : (uint32_t)d.content_type;  // record.rs:173
+              P[b][q >> 2] |= byte << (8 * (q & 3));
+            }
           }
         }
       }
-      uint32_t C[4] = {P[0] ^ k0, P[1] ^ k1, P[2] ^ k2, P[3] ^ k3};
-      if (valid < 16) {  // (data ^ Ek) >> overflow: only `valid` bytes exist
-#pragma unroll
-        for (int w = 0; w < 4; w++) {
-          const int lo = 4 * w;
-          if ((int)valid < lo + 4) C[w] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
-        }
-      }
-      if (valid == 16 && dst_al) {
-        *reinterpret_cast<uint4*>(dst + off) = make_uint4(C[0], C[1], C[2], C[3]);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 16; q++)
-          if ((uint32_t)q < valid) dst[off + q] = (uint8_t)get_byte(C, q);
-      }
-      if (OPEN) {
-        B[0] = P[0]; B[1] = P[1]; B[2] = P[2]; B[3] = P[3];  // GHASH over the ciphertext input
-        if (tls) {
-          const int j = last_nonzero(C, (int)valid);
-          if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((C[j >> 2] >> (8 * (j & 3))) & 0xffu);
-        }
-      } else {
-        B[0] = C[0]; B[1] = C[1]; B[2] = C[2]; B[3] = C[3];
-      }
-    } else {  // length block: [len(A)]_64 || [len(C)]_64 in bits (gcm.rs:121)
-      const uint64_t abits = (uint64_t)(tls ? 5u : aad_len) * 8u, cbits = (uint64_t)n_aead * 8u;
-      B[0] = bswap32((uint32_t)(abits >> 32)); B[1] = bswap32((uint32_t)abits);
-      B[2] = bswap32((uint32_t)(cbits >> 32)); B[3] = bswap32((uint32_t)cbits);
     }
-    ghash_mul_tab(y0, y1, y2, y3, gtab);
-    y0 ^= B[0]; y1 ^= B[1]; y2 ^= B[2]; y3 ^= B[3];
+    aes_encrypt_tt<NR, kNB>(st, rk, rkr, lb);
+#pragma unroll
+    for (int b = 0; b < kNB; b++) {
+      const uint32_t s = base + 64u * b + (uint32_t)lane;
+      if (s == 0) { e0 = st[b][0]; e1 = st[b][1]; e2 = st[b][2]; e3 = st[b][3]; }
+      if (s == 0 || s > m) continue;
+      const uint32_t g = s - 1;
+      uint32_t B[4] = {0, 0, 0, 0};
+      if (g < na) {  // AAD block (gcm.rs:78-87), zero-padded at the end (bytes.rs:110-121)
+        if (tls) {
+          B[0] = hdr0; B[1] = hdr1;
+        } else {
+          const uint32_t off = g * 16;
+#pragma unroll
+          for (int q = 0; q < 16; q++)
+            if (off + q < aad_len) put_byte(B, q, aadp[off + q]);
+        }
+      } else if (g < na + nb) {  // data block (gcm.rs:89-119)
+        const uint32_t off = (g - na) * 16;
+        const uint32_t valid = min(16u, n_aead - off);
+        uint32_t C[4] = {P[b][0] ^ st[b][0], P[b][1] ^ st[b][1], P[b][2] ^ st[b][2], P[b][3] ^ st[b][3]};
+        if (valid < 16) {  // (data ^ Ek) >> overflow: only `valid` bytes exist
+#pragma unroll
+          for (int w = 0; w < 4; w++) {
+            const int lo = 4 * w;
+            if ((int)valid < lo + 4) C[w] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
+          }
+        }
+        if (valid == 16 && fast_dst) {
+          *reinterpret_cast<uint4*>(dst + off) = make_uint4(C[0], C[1], C[2], C[3]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; q++)
+            if ((uint32_t)q < valid) dst[off + q] = (uint8_t)get_byte(C, q);
+        }
+        if (OPEN) {
+#pragma unroll
+          for (int w = 0; w < 4; w++) B[w] = P[b][w];  // GHASH over the ciphertext input
+          if (tls) {
+            const int j = last_nonzero(C, (int)valid);
+            if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((C[j >> 2] >> (8 * (j & 3))) & 0xffu);
+          }
+        } else {
+#pragma unroll
+          for (int w = 0; w < 4; w++) B[w] = C[w];
+        }
+      } else {  // length block: [len(A)]_64 || [len(C)]_64 in bits (gcm.rs:121)
+        const uint64_t abits = (uint64_t)(tls ? 5u : aad_len) * 8u, cbits = (uint64_t)n_aead * 8u;
+        B[0] = bswap32((uint32_t)(abits >> 32)); B[1] = bswap32((uint32_t)abits);
+        B[2] = bswap32((uint32_t)(cbits >> 32)); B[3] = bswap32((uint32_t)cbits);
+      }
+      ghash_mul_tab(y, wb);
+#pragma unroll
+      for (int w = 0; w < 4; w++) y[w] ^= B[w];
+    }
   }
 
   // ---- lane combine: Z = sum_l Y_l * H^(S - s_last(l)) ----
@@ -310,7 +378,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     else if (l <= m) s_last = (int64_t)l + (int64_t)((m - l) / 64) * 64;
     if (s_last >= 1) {
       const uint32_t e = S - (uint32_t)s_last;  // 1..64
-      const uint32_t yb[4] = {bswap32(y0), bswap32(y1), bswap32(y2), bswap32(y3)};
+      const uint32_t yb[4] = {bswap32(y[0]), bswap32(y[1]), bswap32(y[2]), bswap32(y[3])};
       uint32_t hp[4];
 #pragma unroll
       for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e - 1][w];
@@ -361,14 +429,19 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   }
 }
 
-template <bool OPEN>
-__global__ __launch_bounds__(256) void gcm_kernel(GcmArgs A) {
+// WAVES waves per workgroup (one record per wave at a time), one workgroup per CU: the LDS
+// footprint (64 KiB tables + 8 KiB per wave) is what limits residency.
+template <bool OPEN, int kWaves>
+__global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  for (int i = threadIdx.x; i < kTabDwords; i += blockDim.x) smem[i] = A.t0[i >> 5];
+  for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
+    const uint32_t v = A.t0[i >> 6];
+    smem[i] = (i & 32) ? rotl32(v, 8) : v;  // row x: T0[x] in dwords 0..31, T1[x] in 32..63
+  }
   __syncthreads();
   const int wave = (int)uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const uint32_t* T = smem + (lane & 31);
-  uint4* gtab = reinterpret_cast<uint4*>(smem + kTabDwords) + wave * kGhashU4;
+  const uint32_t lb = 4u * (uint32_t)(lane & 31);
+  const uint32_t wb = (uint32_t)kTabBytes + (uint32_t)wave * kGhashBytes;
   const uint32_t stride = gridDim.x * kWaves;
   for (uint32_t r = blockIdx.x * kWaves + wave; r < A.n; r += stride) {
     atls_rec d = A.recs[r];
@@ -399,9 +472,9 @@ __global__ __launch_bounds__(256) void gcm_kernel(GcmArgs A) {
       continue;
     }
     const uint32_t nr = uni(k->valid) ? uni(k->nr) : 0u;
-    if (nr == 10) gcm_record<10, OPEN>(A, d, k, r, T, gtab, lane);
-    else if (nr == 14) gcm_record<14, OPEN>(A, d, k, r, T, gtab, lane);
-    else if (nr == 12) gcm_record<12, OPEN>(A, d, k, r, T, gtab, lane);
+    if (nr == 10) gcm_record<10, OPEN>(A, d, k, r, lb, wb, lane);
+    else if (nr == 14) gcm_record<14, OPEN>(A, d, k, r, lb, wb, lane);
+    else if (nr == 12) gcm_record<12, OPEN>(A, d, k, r, lb, wb, lane);
     else if (lane == 0) {
       atomicOr(A.err, 1u);
       if (OPEN) {
@@ -421,11 +494,21 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                int grid, hipStream_t s) {
   if (n == 0) return 0;
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, err, n_slots};
-  uint32_t want = (n + atls::kWaves - 1) / atls::kWaves;
+  static const int waves = [] {
+    const char* v = getenv("ATLS_GCM_WAVES");
+    const int w = v ? atoi(v) : 12;
+    return (w == 4 || w == 8 || w == 12) ? w : 12;
+  }();
+  uint32_t want = (n + waves - 1) / waves;
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
-  if (open)
-    hipLaunchKernelGGL(atls::gcm_kernel<true>, dim3(g), dim3(256), atls::kLdsBytes, s, A);
-  else
-    hipLaunchKernelGGL(atls::gcm_kernel<false>, dim3(g), dim3(256), atls::kLdsBytes, s, A);
+  const dim3 block(64 * waves);
+  const size_t lds = atls::lds_bytes(waves);
+#define ATLS_LAUNCH(W)                                                                        \
+  if (waves == W) {                                                                           \
+    if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W>), dim3(g), block, lds, s, A);     \
+    else hipLaunchKernelGGL((atls::gcm_kernel<false, W>), dim3(g), block, lds, s, A);         \
+  }
+  ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(12)
+#undef ATLS_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
