@@ -23,7 +23,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libatls.so")
+LIB_PATH = os.environ.get("ATLS_LIB") or os.path.join(_HERE, "libatls.so")  # ATLS_LIB: tuning variants
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"anothertls_amd: {LIB_PATH} is missing; build it with `python -m anothertls_amd._build`")

@@ -18,25 +18,28 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=False):
-    if not force and not _stale():
+def build(force=False, verbose=False, defines=(), out=None):
+    """defines: extra -D flags (kernel tuning variants); out: alternate library path."""
+    lib = out or LIB
+    if not force and not defines and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     objs = []
     for src in SOURCES:
-        obj = os.path.join(CSRC, "_obj", src + ".o")
+        tag = "_".join(d.replace("=", "") for d in defines)
+        obj = os.path.join(CSRC, "_obj", (tag + "_" if tag else "") + src + ".o")
         os.makedirs(os.path.dirname(obj), exist_ok=True)
         lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
-               "-munsafe-fp-atomics", *lang, "-c", os.path.join(CSRC, src), "-o", obj]
+               "-munsafe-fp-atomics", *[f"-D{d}" for d in defines], *lang, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":

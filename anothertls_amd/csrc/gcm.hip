@@ -25,10 +25,18 @@
 
 namespace atls {
 
-constexpr int kNB = 2;                  // independent AES blocks per lane per step (ILP)
-// LDS: [0, 64 KiB) AES tables, row x = 256 B = {T0[x] x32 banks | T1[x] x32 banks}; then one
-// 8 KiB GHASH table per wave. Lane l reads bank (l & 31): conflict-free ds_read_b32.
-constexpr int kTabBytes = 65536;
+#ifndef ATLS_GCM_NB
+#define ATLS_GCM_NB 1
+#endif
+#ifndef ATLS_GCM_NTAB
+#define ATLS_GCM_NTAB 2
+#endif
+constexpr int kNB = ATLS_GCM_NB;      // independent AES blocks per lane per step (ILP)
+constexpr int kNTab = ATLS_GCM_NTAB;  // replicated T-tables in LDS (2: T0,T1; 1: T0 + rotates)
+// LDS: AES tables first. kNTab = 2: row x = 256 B = {T0[x] x32 banks | T1[x] x32 banks} (64 KiB);
+// kNTab = 1: row x = 128 B = T0[x] x32 banks (32 KiB). Then one 8 KiB GHASH table per wave.
+// Lane l reads bank (l & 31): conflict-free ds_read_b32.
+constexpr int kTabBytes = kNTab == 2 ? 65536 : 32768;
 constexpr int kGhashBytes = 8192;
 constexpr size_t lds_bytes(int waves) { return kTabBytes + (size_t)waves * kGhashBytes; }
 
@@ -59,7 +67,8 @@ __device__ __forceinline__ v4u32 lds_u4(uint32_t byte_addr) {
 __device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
   return __builtin_amdgcn_perm(hi, lo, sel);
 }
-#define TA(w, sh) perm((w), lb, 0x0c0c0000u | ((4u + (sh) / 8u) << 8))
+#define TA(w, sh) (kNTab == 2 ? perm((w), lb, 0x0c0c0000u | ((4u + (sh) / 8u) << 8)) \
+                              : ((((w) >> (sh)) & 0xffu) << 7 | lb))
 template <int NR, int NB>
 __device__ __forceinline__ void aes_encrypt_tt(uint32_t (&s)[NB][4], const uint32_t* rk, const uint32_t* rkr,
                                                uint32_t lb) {
@@ -80,8 +89,13 @@ __device__ __forceinline__ void aes_encrypt_tt(uint32_t (&s)[NB][4], const uint3
         const uint32_t bb = (c == 0 ? s1 : c == 1 ? s2 : c == 2 ? s3 : s0);
         const uint32_t cc = (c == 0 ? s2 : c == 1 ? s3 : c == 2 ? s0 : s1);
         const uint32_t dd = (c == 0 ? s3 : c == 1 ? s0 : c == 2 ? s1 : s2);
-        const uint32_t u = xor3(lds_u32(TA(cc, 16)), lds_u32(TA(dd, 24) + 128), rkr[4 * r + c]);
-        t[c] = xor3(lds_u32(TA(a, 0)), lds_u32(TA(bb, 8) + 128), rot16(u));
+        if (kNTab == 2) {
+          const uint32_t u = xor3(lds_u32(TA(cc, 16)), lds_u32(TA(dd, 24) + 128), rkr[4 * r + c]);
+          t[c] = xor3(lds_u32(TA(a, 0)), lds_u32(TA(bb, 8) + 128), rot16(u));
+        } else {
+          const uint32_t u = xor3(lds_u32(TA(cc, 16)), rotl32(lds_u32(TA(dd, 24)), 8), rkr[4 * r + c]);
+          t[c] = xor3(lds_u32(TA(a, 0)), rotl32(lds_u32(TA(bb, 8)), 8), rot16(u));
+        }
       }
 #pragma unroll
       for (int c = 0; c < 4; c++) s[b][c] = t[c];
@@ -100,7 +114,8 @@ __device__ __forceinline__ void aes_encrypt_tt(uint32_t (&s)[NB][4], const uint3
       const uint32_t dd = (c == 0 ? s3 : c == 1 ? s0 : c == 2 ? s1 : s2);
       // {T0[a].b1, T0[b].b1} | {T1[c].b2, T1[d].b3}, then ^ rk: two v_perm + one v_bitop3 ((x|y)^z)
       const uint32_t lo = perm(lds_u32(TA(bb, 8)), lds_u32(TA(a, 0)), 0x0c0c0501u);
-      const uint32_t hi = perm(lds_u32(TA(dd, 24) + 128), lds_u32(TA(cc, 16) + 128), 0x07020c0cu);
+      const uint32_t hi = kNTab == 2 ? perm(lds_u32(TA(dd, 24) + 128), lds_u32(TA(cc, 16) + 128), 0x07020c0cu)
+                                     : perm(lds_u32(TA(dd, 24)), lds_u32(TA(cc, 16)), 0x05010c0cu);
       t[c] = __builtin_amdgcn_bitop3_b32(lo, hi, rk[4 * NR + c], 0x56);
     }
 #pragma unroll
@@ -272,8 +287,41 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0), lane 0
   int64_t lastnz = -1;                      // OPEN+TLS: (pos << 8 | byte) of last non-zero pt byte
   const bool fast_src = src_al, fast_dst = dst_al;
+  // Slots [64*kNB, fast_end) are full 16-byte data blocks that lie wholly inside the input and
+  // output: for them the step below runs branch-free (no classification, no partial handling).
+  const uint32_t full_blocks = min(in_bytes, n_aead) / 16u;
+  const uint32_t fast_end = (src_al && dst_al && is96) ? na + 1u + full_blocks : 0u;
 
   for (uint32_t base = 0; base < S; base += 64 * kNB) {
+    if (base >= 64u * kNB && base + 64u * kNB <= fast_end) {  // wave-uniform
+      uint32_t st[kNB][4];
+      v4u32 P[kNB];
+#pragma unroll
+      for (int b = 0; b < kNB; b++) {
+        const uint32_t s = base + 64u * b + (uint32_t)lane;
+        const uint32_t off = (s - 1u - na) * 16u;
+        P[b] = *reinterpret_cast<const v4u32*>(src + off);
+        st[b][0] = bswap32(j0[0]); st[b][1] = bswap32(j0[1]); st[b][2] = bswap32(j0[2]);
+        st[b][3] = bswap32(j0[3] + (s - na));
+      }
+      aes_encrypt_tt<NR, kNB>(st, rk, rkr, lb);
+#pragma unroll
+      for (int b = 0; b < kNB; b++) {
+        const uint32_t s = base + 64u * b + (uint32_t)lane;
+        const uint32_t off = (s - 1u - na) * 16u;
+        const v4u32 C = {P[b].x ^ st[b][0], P[b].y ^ st[b][1], P[b].z ^ st[b][2], P[b].w ^ st[b][3]};
+        *reinterpret_cast<v4u32*>(dst + off) = C;
+        const v4u32 Bv = OPEN ? P[b] : C;
+        if (OPEN && tls) {
+          const uint32_t cw[4] = {C.x, C.y, C.z, C.w};
+          const int j = last_nonzero(cw, 16);
+          if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((cw[j >> 2] >> (8 * (j & 3))) & 0xffu);
+        }
+        ghash_mul_tab(y, wb);
+        y[0] ^= Bv.x; y[1] ^= Bv.y; y[2] ^= Bv.z; y[3] ^= Bv.w;
+      }
+      continue;
+    }
     uint32_t st[kNB][4];
     uint32_t P[kNB][4];
 #pragma unroll
@@ -435,8 +483,8 @@ template <bool OPEN, int kWaves>
 __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
-    const uint32_t v = A.t0[i >> 6];
-    smem[i] = (i & 32) ? rotl32(v, 8) : v;  // row x: T0[x] in dwords 0..31, T1[x] in 32..63
+    const uint32_t v = A.t0[i >> (kNTab == 2 ? 6 : 5)];
+    smem[i] = (kNTab == 2 && (i & 32)) ? rotl32(v, 8) : v;  // row x: T0[x] x32 (| T1[x] x32)
   }
   __syncthreads();
   const int wave = (int)uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -497,7 +545,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;
-    return (w == 4 || w == 8 || w == 12) ? w : 12;
+    return (w == 4 || w == 8 || w == 12 || (atls::kNTab == 1 && w == 16)) ? w : 12;
   }();
   uint32_t want = (n + waves - 1) / waves;
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
@@ -509,6 +557,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
     else hipLaunchKernelGGL((atls::gcm_kernel<false, W>), dim3(g), block, lds, s, A);         \
   }
   ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(12)
+  if constexpr (atls::kNTab == 1) { ATLS_LAUNCH(16) }
 #undef ATLS_LAUNCH
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
