@@ -1,0 +1,93 @@
+"""CPU check of the bitsliced AES core (anothertls_amd/csrc/aes_bs.h) that the GCM kernel runs
+on the VALU: compiled for the host with software v_bitop3_b32 / v_perm_b32, 32 random blocks
+per key for AES-128/192/256 round keys from the oracle's key expansion, compared against the
+oracle (literal restatement of crypto/aes/cipher.rs) block by block."""
+import os
+import random
+import subprocess
+import tempfile
+
+import oracle as ora
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+SRC = r"""
+#include <stdint.h>
+#include <stdio.h>
+#define __device__
+#define __forceinline__ inline
+static uint32_t __builtin_amdgcn_bitop3_b32(uint32_t a, uint32_t b, uint32_t c, uint32_t tt) {
+  uint32_t r = 0;
+  for (int i = 0; i < 32; i++) {
+    unsigned idx = (((a >> i) & 1) << 2) | (((b >> i) & 1) << 1) | ((c >> i) & 1);
+    r |= ((tt >> idx) & 1u) << i;
+  }
+  return r;
+}
+static uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  uint64_t d = ((uint64_t)s0 << 32) | s1;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; i++) {
+    unsigned b = (sel >> (8 * i)) & 0xff, v;
+    if (b == 12) v = 0; else if (b >= 13) v = 0xff; else v = (d >> (8 * b)) & 0xff;
+    r |= v << (8 * i);
+  }
+  return r;
+}
+#include "aes_bs.h"
+using namespace atls_bs;
+int main(void) {
+  int nr; uint32_t rk[60]; uint32_t blk[4][32];
+  if (scanf("%d", &nr) != 1) return 1;
+  for (int i = 0; i < 4 * (nr + 1); i++) scanf("%x", &rk[i]);
+  for (int k = 0; k < 32; k++) for (int w = 0; w < 4; w++) scanf("%x", &blk[w][k]);
+  uint32_t pl[16][8];
+  for (int w = 0; w < 4; w++) {            // blocks -> planes (transpose is an involution)
+    uint32_t x[32];
+    for (int k = 0; k < 32; k++) x[k] = blk[w][k];
+    transpose32(x);
+    for (int b = 0; b < 4; b++) for (int t = 0; t < 8; t++) pl[4 * w + b][7 - t] = x[8 * b + t];
+  }
+  uint32_t k4[4];
+  for (int c = 0; c < 4; c++) k4[c] = rk[c];
+  add_round_key(pl, k4);
+  for (int r = 1; r < nr; r++) {
+    sub_bytes(pl);
+    for (int c = 0; c < 4; c++) k4[c] = rk[4 * r + c];
+    shift_mix_ark(pl, k4);
+  }
+  sub_bytes(pl);
+  for (int c = 0; c < 4; c++) k4[c] = rk[4 * nr + c];
+  shift_ark(pl, k4);
+  uint32_t out[4][32];
+  planes_to_blocks(pl, out);
+  for (int k = 0; k < 32; k++) { for (int w = 0; w < 4; w++) printf("%08x ", out[w][k]); printf("\n"); }
+  return 0;
+}
+"""
+
+
+def test_bitsliced_aes_matches_oracle():
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.cpp")
+        exe = os.path.join(d, "t")
+        open(c, "w").write(SRC)
+        subprocess.check_call(["g++", "-O1", "-I", os.path.join(ROOT, "anothertls_amd", "csrc"), c, "-o", exe])
+        rng = random.Random(99)
+        for klen in (16, 24, 32):
+            key = bytes(rng.getrandbits(8) for _ in range(klen))
+            nr = klen // 4 + 6
+            ek = bytearray(240)
+            import ctypes
+            buf = (ctypes.c_uint8 * 240)()
+            assert ora.lib().ora_aes_expand_key((ctypes.c_uint8 * klen).from_buffer_copy(key), klen, buf) == 0
+            ek = bytes(buf)
+            rkw = [int.from_bytes(ek[4 * i:4 * i + 4], "little") for i in range(4 * (nr + 1))]
+            blocks = [bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(32)]
+            words = [int.from_bytes(b[4 * w:4 * w + 4], "little") for b in blocks for w in range(4)]
+            inp = f"{nr}\n" + " ".join(f"{x:08x}" for x in rkw) + "\n" + " ".join(f"{x:08x}" for x in words) + "\n"
+            out = subprocess.check_output([exe], input=inp.encode()).decode().split("\n")
+            for k, b in enumerate(blocks):
+                got = b"".join(int(x, 16).to_bytes(4, "little") for x in out[k].split())
+                rc, want = ora.aes_encrypt_block(key, b)
+                assert rc == 0 and got == want, (klen, k)
