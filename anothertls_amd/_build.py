@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libatls.so")
-SOURCES = ["engine.cpp", "keysetup.hip", "gcm.hip", "chacha.hip", "hkdf.hip"]
+SOURCES = ["engine.cpp", "keysetup.hip", "gcm.hip", "gcm_bs.hip", "chacha.hip", "hkdf.hip"]
 ARCH = os.environ.get("ATLS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -24,7 +24,7 @@ def build(force=False, verbose=False, defines=(), out=None):
     if not force and not defines and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    objs = []
+    cmds, objs = [], []
     for src in SOURCES:
         tag = "_".join(d.replace("=", "") for d in defines)
         obj = os.path.join(CSRC, "_obj", (tag + "_" if tag else "") + src + ".o")
@@ -34,8 +34,11 @@ def build(force=False, verbose=False, defines=(), out=None):
                "-munsafe-fp-atomics", *[f"-D{d}" for d in defines], *lang, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
-        subprocess.check_call(cmd)
+        cmds.append(cmd)
         objs.append(obj)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(len(cmds), os.cpu_count() or 1, 8)) as pool:
+        list(pool.map(subprocess.check_call, cmds))
     tmp = lib + ".tmp"
     subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
     os.replace(tmp, lib)

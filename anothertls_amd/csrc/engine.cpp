@@ -25,7 +25,11 @@ extern "C" int atls_launch_key_setup(const atls_key* keys, uint32_t n, void* ks,
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
-                               int grid, hipStream_t s);
+                               int bs_on, int grid, hipStream_t s);
+extern "C" int atls_launch_gcm_bs(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
+                                  const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
+                                  atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
+                                  int nr_mask, int grid, hipStream_t s);
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, uint32_t* err, uint32_t n_slots, int grid,
@@ -63,6 +67,8 @@ struct atls_engine {
   int cus = 256;
   uint32_t n_slots = 0;
   bool has_aes = false, has_chacha = false;  // suites present in the key table: skip idle kernels
+  int aes_nr_mask = 0;                       // bit 0/1/2: AES slots with 10/12/14 rounds
+  bool bitsliced = true;                     // full-size AES-GCM records go to gcm_bs.hip
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
   std::mutex mu;
 };
@@ -144,9 +150,14 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   }
   if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
   int rc = 0;
+  const bool bs = e->has_aes && e->bitsliced && e->aes_nr_mask;
+  if (bs)  // the bitsliced kernels take the full-size records, the T-table kernel the rest
+    rc = atls_launch_gcm_bs(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
+                            (const uint32_t*)e->t0.p, (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask, e->cus * 2, s);
+  if (rc) return rc;
   if (e->has_aes)
     rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
-                         (const uint32_t*)e->t0.p, (uint32_t*)e->err.p, e->n_slots, e->cus * 2, s);
+                         (const uint32_t*)e->t0.p, (uint32_t*)e->err.p, e->n_slots, bs ? 1 : 0, e->cus * 2, s);
   if (rc) return rc;
   if (e->has_chacha)
     rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
@@ -264,6 +275,7 @@ atls_engine* atls_engine_create(int device) {
     return nullptr;
   }
   e->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+  if (const char* v = std::getenv("ATLS_GCM_BS")) e->bitsliced = std::atoi(v) != 0;  // A/B switch
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
       hipStreamSynchronize(e->stream) != hipSuccess) {
     atls_engine_destroy(e);
@@ -308,9 +320,14 @@ int atls_set_keys(atls_engine* e, const atls_key* keys, uint32_t n) {
   if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
   e->n_slots = n;
   e->has_aes = e->has_chacha = false;
+  e->aes_nr_mask = 0;
   for (uint32_t i = 0; i < n; i++) {
-    if (keys[i].suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) e->has_chacha = true;
-    else e->has_aes = true;  // AES-GCM, or an invalid slot the GCM kernel reports
+    if (keys[i].suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) {
+      e->has_chacha = true;
+      continue;
+    }
+    e->has_aes = true;  // AES-GCM, or an invalid slot the GCM kernel reports
+    if (key_status(keys[i]) == ATLS_OK) e->aes_nr_mask |= keys[i].key_len == 16 ? 1 : keys[i].key_len == 24 ? 2 : 4;
   }
   return status;
 }

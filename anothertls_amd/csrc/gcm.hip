@@ -21,7 +21,7 @@
 // Bytes per record (roofline): read L, write L + 16 (tag) -- see DESIGN.md §Roofline.
 #include <cstdlib>
 
-#include "atls_dev.h"
+#include "gcm_common.h"
 
 namespace atls {
 
@@ -40,33 +40,11 @@ constexpr int kTabBytes = kNTab == 2 ? 65536 : 32768;
 constexpr int kGhashBytes = 8192;
 constexpr size_t lds_bytes(int waves) { return kTabBytes + (size_t)waves * kGhashBytes; }
 
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-__device__ __forceinline__ uint32_t rot16(uint32_t x) { return (x << 16) | (x >> 16); }
-
-__device__ __forceinline__ uint32_t lds_u32(uint32_t byte_addr) {
-  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(byte_addr);
-}
-typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ v4u32 lds_u4(uint32_t byte_addr) {
-  return *reinterpret_cast<const __attribute__((address_space(3))) v4u32*>(byte_addr);
-}
-
 // ---- AES (two-table T-table rounds on raw-word state) -------------------------------------
 // T0[x] = {2S,S,S,3S} (LE), T1 = rotl8(T0). With T2 = rotl16(T0), T3 = rotl16(T1):
 //   col_c = T0[s_c.b0] ^ T1[s_{c+1}.b1] ^ rotl16(T0[s_{c+2}.b2] ^ T1[s_{c+3}.b3] ^ rotl16(rk_c)).
 // Table address of byte k of state word w for this lane's bank: (byte << 8) | lb, one v_perm_b32
 // (selector byte 0 <- lb, byte 1 <- w.byte_k, bytes 2-3 <- 0); lb = 4*(lane & 31); T1 at +128.
-__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-  return __builtin_amdgcn_perm(hi, lo, sel);
-}
 #define TA(w, sh) (kNTab == 2 ? perm((w), lb, 0x0c0c0000u | ((4u + (sh) / 8u) << 8)) \
                               : ((((w) >> (sh)) & 0xffu) << 7 | lb))
 template <int NR, int NB>
@@ -123,93 +101,6 @@ __device__ __forceinline__ void aes_encrypt_tt(uint32_t (&s)[NB][4], const uint3
   }
 }
 #undef TA
-
-// ---- GHASH ---------------------------------------------------------------------------------
-// The wave's table at LDS byte address wb: entry [p][n] = (nibble n at position p) * H^64, raw
-// words, p = 2*byte + (low nibble ? 1 : 0) covering x^(4p)..x^(4p+3) (n's bit 3 is x^(4p)).
-// A position's 16 entries x 16 B fill exactly one 256-B bank row: lookups never conflict.
-__device__ __forceinline__ void ghash_build_table(uint32_t wb, const KeySched* k, int lane) {
-  const int p = lane >> 1, half = lane & 1;
-  uint32_t P0[4], P1[4], P2[4], P3[4];
-#pragma unroll
-  for (int w = 0; w < 4; w++) P0[w] = k->p4_be[p][w];
-#pragma unroll
-  for (int w = 0; w < 4; w++) P1[w] = P0[w];
-  gf_mulx_be(P1);
-#pragma unroll
-  for (int w = 0; w < 4; w++) P2[w] = P1[w];
-  gf_mulx_be(P2);
-#pragma unroll
-  for (int w = 0; w < 4; w++) P3[w] = P2[w];
-  gf_mulx_be(P3);
-  uint32_t r0[4], r1[4], r2[4], r3[4];
-#pragma unroll
-  for (int w = 0; w < 4; w++) {
-    r0[w] = bswap32(P0[w]); r1[w] = bswap32(P1[w]); r2[w] = bswap32(P2[w]); r3[w] = bswap32(P3[w]);
-  }
-#pragma unroll
-  for (int j = 0; j < 8; j++) {
-    const int nv = half * 8 + j;
-    uint32_t e[4];
-#pragma unroll
-    for (int w = 0; w < 4; w++)
-      e[w] = ((nv & 8) ? r0[w] : 0u) ^ ((nv & 4) ? r1[w] : 0u) ^ ((nv & 2) ? r2[w] : 0u) ^ ((nv & 1) ? r3[w] : 0u);
-    v4u32 ev = {e[0], e[1], e[2], e[3]};
-    *reinterpret_cast<__attribute__((address_space(3))) v4u32*>(wb + (uint32_t)(p * 256 + nv * 16)) = ev;
-  }
-}
-
-// y <- y * H^64 (raw words) via 32 table lookups. Each nibble's table offset (n * 16) is the
-// nibble's byte of (y & 0xF0F0F0F0) or ((y << 4) & 0xF0F0F0F0), OR-ed onto the wave base.
-__device__ __forceinline__ void ghash_mul_tab(uint32_t (&y)[4], uint32_t wb) {
-  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t hi4 = y[i] & 0xF0F0F0F0u, lo4 = (y[i] << 4) & 0xF0F0F0F0u;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const uint32_t byte = 4 * i + b;
-      // address = wb | (nibble << 4): byte 0 from the nibble's byte, bytes 1-2 from wb (one v_perm)
-      const uint32_t sel = 0x0c020100u | (4u + b);
-      const v4u32 eh = lds_u4(perm(hi4, wb, sel) + (2 * byte) * 256);
-      const v4u32 el = lds_u4(perm(lo4, wb, sel) + (2 * byte + 1) * 256);
-      a0 = xor3(a0, eh.x, el.x); a1 = xor3(a1, eh.y, el.y); a2 = xor3(a2, eh.z, el.z); a3 = xor3(a3, eh.w, el.w);
-    }
-  }
-  y[0] = a0; y[1] = a1; y[2] = a2; y[3] = a3;
-}
-
-// ---- byte helpers for partial / unaligned blocks -------------------------------------------
-__device__ __forceinline__ void put_byte(uint32_t w[4], int q, uint32_t v) { w[q >> 2] |= v << (8 * (q & 3)); }
-__device__ __forceinline__ uint32_t get_byte(const uint32_t w[4], int q) { return (w[q >> 2] >> (8 * (q & 3))) & 0xffu; }
-
-// Highest non-zero byte index (< valid) of a raw block, or -1.
-__device__ __forceinline__ int last_nonzero(const uint32_t w[4], int valid) {
-  int r = -1;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    uint32_t x = w[i];
-    const int lo = 4 * i;
-    if (valid < lo + 4) x &= (valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
-    if (x) r = lo + (31 - __builtin_clz(x)) / 8;
-  }
-  return r;
-}
-
-struct GcmArgs {
-  const KeySched* ks;
-  const atls_rec* recs;
-  uint32_t n;
-  const uint8_t* in;
-  const uint8_t* aux;
-  uint8_t* out;
-  uint8_t* tags_out;       // seal
-  const uint8_t* tags_in;  // open
-  atls_open_result* res;   // open
-  const uint32_t* t0;      // 256-entry T-table in global memory
-  uint32_t* err;           // sticky error word
-  uint32_t n_slots;        // key-table size: descriptors are bounds-checked on the device
-};
 
 template <int NR, bool OPEN>
 __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx,
@@ -280,7 +171,12 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   const uint32_t S = m + 1u;        // slots: E(J0) + GHASH blocks
   const uint32_t in_bytes = len;    // bytes readable from src
 
-  ghash_build_table(wb, k, lane);
+  {
+    uint32_t seed[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) seed[w] = k->p4_be[lane >> 1][w];
+    ghash_table_entries<8>(wb, seed, lane >> 1, (lane & 1) * 8);
+  }
   wave_lds_sync();
 
   uint32_t y[4] = {0, 0, 0, 0};
@@ -455,24 +351,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     if (lane == 0) {
       const uint32_t* tg = reinterpret_cast<const uint32_t*>(A.tags_in + 16ull * rec_idx);
       const bool ok = (tg[0] == t0) & (tg[1] == t1) & (tg[2] == t2) & (tg[3] == t3);
-      atls_open_result r;
-      r.reserved[0] = r.reserved[1] = 0;
-      if (!tls) {
-        r.status = ok ? ATLS_OK : ATLS_BAD_RECORD_MAC;
-        r.content_len = len;
-        r.content_type = 0;
-      } else if (!ok) {
-        r.status = ATLS_DECRYPT_ERROR;
-        r.content_len = 0;
-        r.content_type = 0;
-      } else {
-        const uint32_t ty = lastnz >= 0 ? (uint32_t)(lastnz & 0xff) : 0u;
-        const bool valid_type = ty == 0 || ty == 20 || ty == 21 || ty == 22 || ty == 23;
-        r.status = valid_type ? ATLS_OK : ATLS_DECODE_ERROR;
-        r.content_len = (valid_type && lastnz >= 0) ? (uint32_t)(lastnz >> 8) : 0u;
-        r.content_type = valid_type ? (uint8_t)ty : 0;
-      }
-      A.res[rec_idx] = r;
+      write_open_result(A, rec_idx, tls, len, ok, lastnz);
     }
   }
 }
@@ -492,6 +371,7 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   const uint32_t wb = (uint32_t)kTabBytes + (uint32_t)wave * kGhashBytes;
   const uint32_t stride = gridDim.x * kWaves;
   for (uint32_t r = blockIdx.x * kWaves + wave; r < A.n; r += stride) {
+    if (uni(bs_taken<OPEN>(A, r))) continue;  // gcm_bs.hip seals / opens this one
     atls_rec d = A.recs[r];
     d.key_slot = uni(d.key_slot);
     d.len = uni(d.len);
@@ -539,9 +419,10 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
-                               int grid, hipStream_t s) {
+                               int bs_on, int grid, hipStream_t s) {
   if (n == 0) return 0;
-  atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, err, n_slots};
+  atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, err, n_slots,
+                  (uint32_t)(bs_on != 0)};
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;

@@ -1,0 +1,188 @@
+// Pieces shared by the two AES-GCM record kernels (gcm.hip: T-table AES, one record per wave;
+// gcm_bs.hip: bitsliced AES, two records per wave): LDS/VALU helpers, the 4-bit GHASH tables,
+// byte helpers for partial blocks, the kernel argument block, and the rule that splits a
+// batch between the two kernels.
+#pragma once
+#include "atls_dev.h"
+
+namespace atls {
+
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t rot16(uint32_t x) { return (x << 16) | (x >> 16); }
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// Read-only data (key schedules, descriptors) through the constant address space: loads from a
+// wave-uniform address become scalar loads into SGPRs.
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(4))) T* cptr(const T* p) {
+  return (const __attribute__((address_space(4))) T*)(p);
+}
+
+__device__ __forceinline__ uint32_t lds_u32(uint32_t byte_addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) uint32_t*>(byte_addr);
+}
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4u32 lds_u4(uint32_t byte_addr) {
+  return *reinterpret_cast<const __attribute__((address_space(3))) v4u32*>(byte_addr);
+}
+
+// ---- GHASH ---------------------------------------------------------------------------------
+// A table at LDS byte address wb (256-B aligned, < 2^24): entry [p][n] = (nibble n at position
+// p) * H^e, raw words, p = 2*byte + (low nibble ? 1 : 0) covering x^(4p)..x^(4p+3) (n's bit 3
+// is x^(4p)). A position's 16 entries x 16 B fill exactly one 256-B bank row, so lookups never
+// bank-conflict. This writes entries n0 .. n0+CNT-1 of position p from seed = x^(4p) * H^e.
+template <int CNT>
+__device__ __forceinline__ void ghash_table_entries(uint32_t wb, const uint32_t (&seed_be)[4], int p, int n0) {
+  uint32_t P0[4], P1[4], P2[4], P3[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) P0[w] = seed_be[w];
+#pragma unroll
+  for (int w = 0; w < 4; w++) P1[w] = P0[w];
+  gf_mulx_be(P1);
+#pragma unroll
+  for (int w = 0; w < 4; w++) P2[w] = P1[w];
+  gf_mulx_be(P2);
+#pragma unroll
+  for (int w = 0; w < 4; w++) P3[w] = P2[w];
+  gf_mulx_be(P3);
+  uint32_t r0[4], r1[4], r2[4], r3[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) {
+    r0[w] = bswap32(P0[w]); r1[w] = bswap32(P1[w]); r2[w] = bswap32(P2[w]); r3[w] = bswap32(P3[w]);
+  }
+#pragma unroll
+  for (int j = 0; j < CNT; j++) {
+    const int nv = n0 + j;
+    uint32_t e[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+      e[w] = ((nv & 8) ? r0[w] : 0u) ^ ((nv & 4) ? r1[w] : 0u) ^ ((nv & 2) ? r2[w] : 0u) ^ ((nv & 1) ? r3[w] : 0u);
+    v4u32 ev = {e[0], e[1], e[2], e[3]};
+    *reinterpret_cast<__attribute__((address_space(3))) v4u32*>(wb + (uint32_t)(p * 256 + nv * 16)) = ev;
+  }
+}
+
+// y <- y * H^e (raw words) via 32 table lookups. Each nibble's table offset (n * 16) is the
+// nibble's byte of (y & 0xF0F0F0F0) or ((y << 4) & 0xF0F0F0F0), OR-ed onto the table base.
+// GROUPED: lookups go out 8 at a time (32 VGPRs in flight instead of up to 128).
+template <bool GROUPED = false>
+__device__ __forceinline__ void ghash_mul_tab(uint32_t (&y)[4], uint32_t wb) {
+  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t hi4 = y[i] & 0xF0F0F0F0u, lo4 = (y[i] << 4) & 0xF0F0F0F0u;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t byte = 4 * i + b;
+      // address = wb | (nibble << 4): byte 0 from the nibble's byte, bytes 1-2 from wb (one v_perm)
+      const uint32_t sel = 0x0c020100u | (4u + b);
+      const v4u32 eh = lds_u4(perm(hi4, wb, sel) + (2 * byte) * 256);
+      const v4u32 el = lds_u4(perm(lo4, wb, sel) + (2 * byte + 1) * 256);
+      a0 = xor3(a0, eh.x, el.x); a1 = xor3(a1, eh.y, el.y); a2 = xor3(a2, eh.z, el.z); a3 = xor3(a3, eh.w, el.w);
+    }
+    if (GROUPED) __builtin_amdgcn_sched_barrier(0);
+  }
+  y[0] = a0; y[1] = a1; y[2] = a2; y[3] = a3;
+}
+
+// ---- byte helpers for partial / unaligned blocks -------------------------------------------
+__device__ __forceinline__ void put_byte(uint32_t w[4], int q, uint32_t v) { w[q >> 2] |= v << (8 * (q & 3)); }
+__device__ __forceinline__ uint32_t get_byte(const uint32_t w[4], int q) { return (w[q >> 2] >> (8 * (q & 3))) & 0xffu; }
+
+// Highest non-zero byte index (< valid) of a raw block, or -1.
+__device__ __forceinline__ int last_nonzero(const uint32_t w[4], int valid) {
+  int r = -1;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint32_t x = w[i];
+    const int lo = 4 * i;
+    if (valid < lo + 4) x &= (valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
+    if (x) r = lo + (31 - __builtin_clz(x)) / 8;
+  }
+  return r;
+}
+
+struct GcmArgs {
+  const KeySched* ks;
+  const atls_rec* recs;
+  uint32_t n;
+  const uint8_t* in;
+  const uint8_t* aux;
+  uint8_t* out;
+  uint8_t* tags_out;       // seal
+  const uint8_t* tags_in;  // open
+  atls_open_result* res;   // open
+  const uint32_t* t0;      // 256-entry T-table in global memory
+  uint32_t* err;           // sticky error word
+  uint32_t n_slots;        // key-table size: descriptors are bounds-checked on the device
+  uint32_t bs_on;          // 1: records bs_taken() accepts go to the bitsliced kernel
+};
+
+// Open result for one record (record.rs:203-240 decrypt + padding scan). lastnz = (position <<
+// 8 | byte) of the last non-zero plaintext byte, -1 if none.
+__device__ __forceinline__ void write_open_result(const GcmArgs& A, uint32_t rec_idx, bool tls, uint32_t len, bool ok,
+                                                  int64_t lastnz) {
+  atls_open_result r;
+  r.reserved[0] = r.reserved[1] = 0;
+  if (!tls) {
+    r.status = ok ? ATLS_OK : ATLS_BAD_RECORD_MAC;
+    r.content_len = len;
+    r.content_type = 0;
+  } else if (!ok) {
+    r.status = ATLS_DECRYPT_ERROR;
+    r.content_len = 0;
+    r.content_type = 0;
+  } else {
+    const uint32_t ty = lastnz >= 0 ? (uint32_t)(lastnz & 0xff) : 0u;
+    const bool valid_type = ty == 0 || ty == 20 || ty == 21 || ty == 22 || ty == 23;
+    r.status = valid_type ? ATLS_OK : ATLS_DECODE_ERROR;
+    r.content_len = (valid_type && lastnz >= 0) ? (uint32_t)(lastnz >> 8) : 0u;
+    r.content_type = valid_type ? (uint8_t)ty : 0;
+  }
+  A.res[rec_idx] = r;
+}
+
+// ---- batch split between the kernels --------------------------------------------------------
+// The bitsliced kernel runs whole 1024-block passes (32 lanes x 32 blocks) per record. A
+// record qualifies when those passes hold only full, aligned data blocks (plus E_K(J0)), the
+// few blocks after them (<= 2 per lane: partial block, length block) fit the scalar tail, the
+// nonce is 96-bit and the AAD is at most 32 blocks. Returns the AES round count, 0 if not.
+constexpr uint32_t kBsPass = 1024;
+template <bool OPEN>
+__device__ __forceinline__ uint32_t bs_class(const GcmArgs& A, const atls_rec& d) {
+  if (d.key_slot >= A.n_slots || d.mode > ATLS_MODE_RAW) return 0;
+  const KeySched* k = A.ks + d.key_slot;
+  if (!k->valid || (k->suite != (uint32_t)kSuiteAes128 && k->suite != (uint32_t)kSuiteAes256)) return 0;
+  const bool tls = d.mode == ATLS_MODE_TLS;
+  if (!tls && (d.iv_len != 12 || d.aad_len > 512)) return 0;
+  const uint32_t n_aead = (tls && !OPEN) ? d.len + 1 : d.len;
+  const uint32_t full = d.len / 16u;  // min(len, n_aead) / 16
+  const uint32_t passes = (full + 1u) / kBsPass;
+  if (passes == 0) return 0;
+  const uint32_t nb = (n_aead + 15u) / 16u;
+  if (nb + 2u - kBsPass * passes > 64u) return 0;
+  if (((uintptr_t)(A.in + d.in_off) | (uintptr_t)(A.out + d.out_off)) & 15u) return 0;
+  return k->nr;
+}
+// Records are paired (2q, 2q+1) onto one wave; a pair runs one round count, so the odd record
+// of a pair whose even record takes a different one is left to the T-table kernel.
+template <bool OPEN>
+__device__ __forceinline__ uint32_t bs_taken(const GcmArgs& A, uint32_t r) {
+  if (!A.bs_on) return 0;
+  const uint32_t c = bs_class<OPEN>(A, A.recs[r]);
+  if (c == 0 || (r & 1u) == 0) return c;
+  const uint32_t c0 = bs_class<OPEN>(A, A.recs[r - 1]);
+  return (c0 != 0 && c0 != c) ? 0u : c;
+}
+
+}  // namespace atls

@@ -3,7 +3,7 @@
 // reference does (gcm.rs:52-56 re-expands the key and recomputes H on every call):
 //   * AES round keys (crypto/aes/cipher.rs:216-249) as raw words for the T-table rounds;
 //   * H = E_K(0^128) (gcm.rs:56), H^1..H^64 (lane-combine multipliers), and
-//     x^(4p)*H^64 for p = 0..31 (seeds of the per-record 4-bit GHASH tables);
+//     x^(4p)*H^64 and x^(4p)*H^32 for p = 0..31 (seeds of the per-record 4-bit GHASH tables);
 //   * ChaCha20 key words (chacha20/cipher.rs:29-31).
 // Also builds the 256-entry AES T-table T0 used (replicated per LDS bank) by gcm.hip.
 #include "atls_dev.h"
@@ -125,6 +125,12 @@ __global__ void key_setup_kernel(const atls_key* __restrict__ keys, uint32_t n, 
   uint32_t v[4] = {o->hpow_be[63][0], o->hpow_be[63][1], o->hpow_be[63][2], o->hpow_be[63][3]};
   for (int j = 0; j < 32; j++) {
     for (int w = 0; w < 4; w++) o->p4_be[j][w] = v[w];
+    gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v);
+  }
+  // p4h32[j] = x^(4j) * H^32
+  for (int w = 0; w < 4; w++) v[w] = o->hpow_be[31][w];
+  for (int j = 0; j < 32; j++) {
+    for (int w = 0; w < 4; w++) o->p4h32_be[j][w] = v[w];
     gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v);
   }
   o->valid = 1;
