@@ -1,26 +1,25 @@
-// Bitsliced AES for gfx950: 32 blocks per lane, one bit of each block per bit of a 32-bit
-// plane, AES rounds as v_bitop3_b32 / v_perm_b32 logic on the VALU (no table lookups).
+// Bitsliced AES for gfx950: 32 blocks per lane, AES rounds as v_bitop3_b32 / v_perm_b32 /
+// v_alignbit_b32 logic on the VALU (no table lookups).
 //
-// State: pl[i][j] = plane of state byte i (i = 4*column + row, FIPS-197 order), bit (7 - j):
-// j = 0 is the byte's most significant bit (the S-box circuit's U0). Bit k of every plane is
-// block k. Round keys enter as the raw little-endian words of the 16 round-key bytes (the
-// layout of KeySched::rk, crypto/aes/cipher.rs:216-249 expanded_key); each key bit becomes an
-// all-zeros / all-ones plane mask (Key1: one key per lane; Key2: two keys, one per 16 blocks).
+// Row-plane layout: st[g][r][j], g = block group (blocks 8g..8g+7), r = state row, j = bit
+// significance 7 - j (j = 0 is the MSB, the S-box circuit's U0). Bit 8c + b of a word is bit
+// (7 - j) of state byte (row r, column c) -- FIPS-197 byte 4c + r -- of block 8g + b. So
+//   * SubBytes is the 94-op circuit (sbox_bs.h) on the 8 words of each (g, r): 32 bytes at once;
+//   * ShiftRows rotates row r's words right by 8r bits (one v_alignbit each), in place;
+//   * MixColumns combines the four row words of a (g, significance) -- all columns aligned;
+//   * AddRoundKey XORs 32 mask words per round (byte c of mask (r, j) = 0xFF where round-key
+//     byte (r, c) has bit 7 - j), shared by the four groups; one v_perm_b32 builds a mask from
+//     pre-packed key words using v_perm's sign-replicating selectors.
+// The layout never renames registers, so a rolled round loop keeps its 128 state words in place.
+// Round keys are the raw little-endian words of the 16 round-key bytes (KeySched::rk layout,
+// crypto/aes/cipher.rs:216-249 expanded_key): word c = column c, byte r = row r.
 //
 // Host-compilable (tests/test_aes_bs_emulation.py runs it on the CPU with software versions of
-// __builtin_amdgcn_bitop3_b32 and __builtin_amdgcn_perm).
+// __builtin_amdgcn_bitop3_b32, __builtin_amdgcn_perm and __builtin_amdgcn_alignbit).
 #pragma once
 #include <stdint.h>
 
 #include "sbox_bs.h"
-
-// Scheduling fence: keeps the machine scheduler from interleaving independent S-boxes /
-// columns, which multiplies live temporaries past the 256-VGPR budget of two waves per SIMD.
-#if defined(__HIP_DEVICE_COMPILE__) && defined(ATLS_BS_FENCES)
-#define ATLS_BS_FENCE() __builtin_amdgcn_sched_barrier(0)
-#else
-#define ATLS_BS_FENCE() ((void)0)
-#endif
 
 namespace atls_bs {
 
@@ -29,90 +28,91 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 }
 // bit `b` of w -> 0 or 0xffffffff
 __device__ __forceinline__ uint32_t bmask(uint32_t w, int b) { return (uint32_t)((int32_t)(w << (31 - b)) >> 31); }
+__device__ __forceinline__ uint32_t rotr(uint32_t w, int n) { return n ? __builtin_amdgcn_alignbit(w, w, n) : w; }
 
-// Round-key masks. Key1: one key for all 32 blocks of the lane. Key2: key `a` for blocks 0-15
-// (plane bits 0-15), key `b` for blocks 16-31 -- when a and b are wave-uniform the masks are
-// scalar (SALU) values and every AddRoundKey XOR folds into a VALU op's SGPR operand.
-struct Key1 {
-  uint32_t w[4];
-  __device__ __forceinline__ uint32_t mask(int c, int bit) const { return bmask(w[c], bit); }
-};
-struct Key2 {
-  uint32_t a[4], b[4];
-  __device__ __forceinline__ uint32_t mask(int c, int bit) const {
-    return (bmask(a[c], bit) & 0x0000ffffu) | (bmask(b[c], bit) << 16);  // s_pack_ll_b32_b16
-  }
-};
+typedef uint32_t State[4][4][8];  // [group][row][significance 7 - j]
+typedef uint32_t Masks[4][8];     // [row][significance 7 - j]
 
-__device__ __forceinline__ void sub_bytes(uint32_t (&pl)[16][8]) {
+// Round-key masks from the four raw key words (or any four column words, e.g. a nonce XOR key).
+// For bit p = 8r + t: S1 carries bit p of w0 / w1 at bits 15 / 31, S0 bit p of w2 / w3 at bits
+// 15 / 31, and v_perm selectors 8..11 replicate exactly those four bits into bytes 0..3.
+__device__ __forceinline__ void make_masks(const uint32_t (&w)[4], Masks& m) {
+  const uint32_t lo01 = __builtin_amdgcn_perm(w[1], w[0], 0x05040100u);  // {w0.lo16, w1.lo16}
+  const uint32_t lo23 = __builtin_amdgcn_perm(w[3], w[2], 0x05040100u);
+  const uint32_t hi01 = __builtin_amdgcn_perm(w[1], w[0], 0x07060302u);  // {w0.hi16, w1.hi16}
+  const uint32_t hi23 = __builtin_amdgcn_perm(w[3], w[2], 0x07060302u);
 #pragma unroll
-  for (int i = 0; i < 16; i++) {
-    sbox_bs(pl[i]);
-    ATLS_BS_FENCE();
-  }
-}
-
-// ShiftRows + MixColumns + AddRoundKey. rk[c] = raw word of round-key column c (byte r = row r).
-// out_r = xtime(a_r ^ a_{r+1}) ^ a_{r+1} ^ a_{r+2} ^ a_{r+3} (+ key), a_r = ShiftRows input
-// byte (row r, column c + r). Planes are MSB-first: significance t lives at index 7 - t.
-template <class KM>
-__device__ __forceinline__ void shift_mix_ark(uint32_t (&pl)[16][8], const KM& km) {
-  uint32_t o[16][8];
+  for (int r = 0; r < 4; r++)
 #pragma unroll
-  for (int c = 0; c < 4; c++) {
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const uint32_t* a0 = pl[4 * ((c + r) & 3) + r];
-      const uint32_t* a1 = pl[4 * ((c + r + 1) & 3) + ((r + 1) & 3)];
-      const uint32_t* a2 = pl[4 * ((c + r + 2) & 3) + ((r + 2) & 3)];
-      const uint32_t* a3 = pl[4 * ((c + r + 3) & 3) + ((r + 3) & 3)];
-      uint32_t u[8], v[8];  // indexed by significance t
-#pragma unroll
-      for (int t = 0; t < 8; t++) {
-        u[t] = a0[7 - t] ^ a1[7 - t];
-        v[t] = xor3(a1[7 - t], a2[7 - t], a3[7 - t]);
-      }
-#pragma unroll
-      for (int t = 0; t < 8; t++) {
-        const uint32_t k = km.mask(c, 8 * r + t);
-        uint32_t x;
-        if (t == 0) x = xor3(v[0], u[7], k);
-        else if (t == 1 || t == 3 || t == 4) x = xor3(xor3(v[t], u[t - 1], u[7]), k, 0u);
-        else x = xor3(v[t], u[t - 1], k);
-        o[4 * c + r][7 - t] = x;
-      }
+    for (int t = 0; t < 8; t++) {
+      const int p = 8 * r + t;
+      const uint32_t s1 = p < 16 ? lo01 << (15 - p) : hi01 << (31 - p);
+      const uint32_t s0 = p < 16 ? lo23 << (15 - p) : hi23 << (31 - p);
+      m[r][7 - t] = __builtin_amdgcn_perm(s0, s1, 0x0b0a0908u);
     }
-    ATLS_BS_FENCE();
-  }
-#pragma unroll
-  for (int i = 0; i < 16; i++)
-#pragma unroll
-    for (int j = 0; j < 8; j++) pl[i][j] = o[i][j];
 }
 
-// Final round: ShiftRows + AddRoundKey (no MixColumns).
-template <class KM>
-__device__ __forceinline__ void shift_ark(uint32_t (&pl)[16][8], const KM& km) {
-  uint32_t o[16][8];
+__device__ __forceinline__ void sub_bytes(State& st) {
 #pragma unroll
-  for (int c = 0; c < 4; c++)
+  for (int g = 0; g < 4; g++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) sbox_bs(st[g][r]);
+}
+
+__device__ __forceinline__ void add_round_key(State& st, const Masks& m) {
+#pragma unroll
+  for (int g = 0; g < 4; g++)
 #pragma unroll
     for (int r = 0; r < 4; r++)
 #pragma unroll
-      for (int j = 0; j < 8; j++) o[4 * c + r][j] = pl[4 * ((c + r) & 3) + r][j] ^ km.mask(c, 8 * r + 7 - j);
-  ATLS_BS_FENCE();
-#pragma unroll
-  for (int i = 0; i < 16; i++)
-#pragma unroll
-    for (int j = 0; j < 8; j++) pl[i][j] = o[i][j];
+      for (int j = 0; j < 8; j++) st[g][r][j] ^= m[r][j];
 }
 
-template <class KM>
-__device__ __forceinline__ void add_round_key(uint32_t (&pl)[16][8], const KM& km) {
+// ShiftRows + MixColumns + AddRoundKey. After ShiftRows a_r = row r of the column;
+// out_r = xtime(a_r ^ a_{r+1}) ^ a_{r+1} ^ a_{r+2} ^ a_{r+3} ^ key. xtime puts bit t-1 of
+// u = a_r ^ a_{r+1} at bit t and folds u's bit 7 into bits 0, 1, 3, 4 (0x1b). Significances are
+// rewritten in place from 7 down to 0, so each step reads only not-yet-written lower bits; u's
+// bit 7 is saved first. Temporaries: 4 + 4 words per group.
+__device__ __forceinline__ void shift_mix_ark(State& st, const Masks& m) {
 #pragma unroll
-  for (int i = 0; i < 16; i++)
+  for (int g = 0; g < 4; g++) {
+    uint32_t (&a)[4][8] = st[g];  // a[r][7 - t]
 #pragma unroll
-    for (int j = 0; j < 8; j++) pl[i][j] ^= km.mask(i >> 2, 8 * (i & 3) + 7 - j);
+    for (int r = 1; r < 4; r++)
+#pragma unroll
+      for (int j = 0; j < 8; j++) a[r][j] = rotr(a[r][j], 8 * r);
+    uint32_t u7[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) u7[r] = a[r][0] ^ a[(r + 1) & 3][0];
+#pragma unroll
+    for (int t = 7; t >= 0; t--) {
+      const int j = 7 - t;
+      uint32_t o[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const uint32_t v = xor3(a[(r + 1) & 3][j], a[(r + 2) & 3][j], a[(r + 3) & 3][j]);
+        const uint32_t k = m[r][j];
+        if (t == 0) {
+          o[r] = xor3(v, u7[r], k);
+        } else {
+          const uint32_t u = a[r][j + 1] ^ a[(r + 1) & 3][j + 1];  // bit t - 1 of a_r ^ a_{r+1}
+          o[r] = (t == 1 || t == 3 || t == 4) ? xor3(xor3(v, u, u7[r]), k, 0u) : xor3(v, u, k);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) a[r][j] = o[r];
+    }
+  }
+}
+
+// Final round: ShiftRows + AddRoundKey (no MixColumns).
+__device__ __forceinline__ void shift_ark(State& st, const Masks& m) {
+#pragma unroll
+  for (int g = 0; g < 4; g++)
+#pragma unroll
+    for (int r = 0; r < 4; r++)
+#pragma unroll
+      for (int j = 0; j < 8; j++) st[g][r][j] = rotr(st[g][r][j], 8 * r) ^ m[r][j];
 }
 
 // Rows i and i + S (i & S == 0) exchange the bit columns selected by ~m and m respectively.
@@ -151,22 +151,23 @@ __device__ __forceinline__ void transpose32(uint32_t (&x)[32]) {
   delta_swaps<1>(x, 0x55555555u);
 }
 
-// Planes -> 32 blocks: blk[w][k] = raw word w (bytes 4w..4w+3, little-endian) of block k.
-// Group w's 32 rows are ordered p = 8*byte_in_word + significance, so after the transpose row k
-// holds word w of block k. The result overwrites pl (viewed as 4 x 32 words).
-__device__ __forceinline__ void planes_to_blocks(uint32_t (&pl)[16][8], uint32_t (&blk)[4][32]) {
+// Group g's 32 words -> its 8 blocks: rows ordered 8r + t; after the transpose x[8c + b] is raw
+// word c (column c, byte r = row r) of block 8g + b.
+__device__ __forceinline__ void group_to_blocks(const uint32_t (&grp)[4][8], uint32_t (&x)[32]) {
 #pragma unroll
-  for (int w = 0; w < 4; w++) {
-    uint32_t x[32];
+  for (int r = 0; r < 4; r++)
 #pragma unroll
-    for (int b = 0; b < 4; b++)
+    for (int t = 0; t < 8; t++) x[8 * r + t] = grp[r][7 - t];
+  transpose32(x);
+}
+
+// The inverse (blocks -> planes, for tests): x[8c + b] = raw word c of block 8g + b.
+__device__ __forceinline__ void blocks_to_group(uint32_t (&x)[32], uint32_t (&grp)[4][8]) {
+  transpose32(x);
 #pragma unroll
-      for (int t = 0; t < 8; t++) x[8 * b + t] = pl[4 * w + b][7 - t];
-    transpose32(x);
+  for (int r = 0; r < 4; r++)
 #pragma unroll
-    for (int k = 0; k < 32; k++) blk[w][k] = x[k];
-    ATLS_BS_FENCE();
-  }
+    for (int t = 0; t < 8; t++) grp[r][7 - t] = x[8 * r + t];
 }
 
 }  // namespace atls_bs

@@ -68,7 +68,7 @@ struct atls_engine {
   uint32_t n_slots = 0;
   bool has_aes = false, has_chacha = false;  // suites present in the key table: skip idle kernels
   int aes_nr_mask = 0;                       // bit 0/1/2: AES slots with 10/12/14 rounds
-  bool bitsliced = true;                     // full-size AES-GCM records go to gcm_bs.hip
+  bool bitsliced = false;                    // ATLS_GCM_BS=1: full-size AES-GCM records go to gcm_bs.hip
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
   std::mutex mu;
 };

@@ -74,8 +74,9 @@ __device__ __forceinline__ void ghash_table_entries(uint32_t wb, const uint32_t 
 
 // y <- y * H^e (raw words) via 32 table lookups. Each nibble's table offset (n * 16) is the
 // nibble's byte of (y & 0xF0F0F0F0) or ((y << 4) & 0xF0F0F0F0), OR-ed onto the table base.
-// GROUPED: lookups go out 8 at a time (32 VGPRs in flight instead of up to 128).
-template <bool GROUPED = false>
+// GROUP > 0: lookups go out GROUP at a time (4*GROUP VGPRs in flight instead of up to 128), each
+// group followed by a scheduling fence.
+template <int GROUP = 0>
 __device__ __forceinline__ void ghash_mul_tab(uint32_t (&y)[4], uint32_t wb) {
   uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
 #pragma unroll
@@ -90,7 +91,31 @@ __device__ __forceinline__ void ghash_mul_tab(uint32_t (&y)[4], uint32_t wb) {
       const v4u32 el = lds_u4(perm(lo4, wb, sel) + (2 * byte + 1) * 256);
       a0 = xor3(a0, eh.x, el.x); a1 = xor3(a1, eh.y, el.y); a2 = xor3(a2, eh.z, el.z); a3 = xor3(a3, eh.w, el.w);
     }
-    if (GROUPED) __builtin_amdgcn_sched_barrier(0);
+    if (GROUP > 0 && ((i + 1) * 8) % GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+  }
+  y[0] = a0; y[1] = a1; y[2] = a2; y[3] = a3;
+}
+
+// The same product with W lookups issued before their first use (4W VGPRs in flight): 32 / W
+// LDS round trips per multiply, where the compiler alone waits after every few lookups.
+template <int W>
+__device__ __forceinline__ void ghash_mul_tab_wide(uint32_t (&y)[4], uint32_t wb) {
+  uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+#pragma unroll
+  for (int g = 0; g < 32; g += W) {
+    v4u32 e[W];
+#pragma unroll
+    for (int q = 0; q < W; q++) {
+      const int byte = (g + q) >> 1, i = byte >> 2, b = byte & 3;
+      const uint32_t nib4 = ((g + q) & 1) ? (y[i] << 4) & 0xF0F0F0F0u : y[i] & 0xF0F0F0F0u;
+      e[q] = lds_u4(perm(nib4, wb, 0x0c020100u | (4u + b)) + (g + q) * 256);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < W; q += 2) {
+      a0 = xor3(a0, e[q].x, e[q + 1].x); a1 = xor3(a1, e[q].y, e[q + 1].y);
+      a2 = xor3(a2, e[q].z, e[q + 1].z); a3 = xor3(a3, e[q].w, e[q + 1].w);
+    }
   }
   y[0] = a0; y[1] = a1; y[2] = a2; y[3] = a3;
 }

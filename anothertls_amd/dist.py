@@ -1,0 +1,70 @@
+"""One process per GPU: rendezvous, sharding and whole-job timing for batch sealing.
+
+Records are independent, so a multi-GPU job is N copies of the single-GPU path over disjoint
+shards of the record stream (workload.shard_batch): no collective touches the data. The only
+collectives are the barriers around the timed region and one max-reduce of the wall time
+(torch.distributed; backend "nccl" = RCCL on ROCm between GPUs, "gloo" for CPU tests).
+"""
+import os
+import time
+
+import torch
+import torch.distributed as tdist
+
+
+def env_ranks():
+    """(rank, local_rank, world_size) from the torch.distributed.run environment."""
+    return int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+
+
+def init(backend, device=None):
+    """Join the process group (MASTER_ADDR defaults to 127.0.0.1). No-op for a single rank."""
+    _, _, world = env_ranks()
+    if world <= 1:
+        return False
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
+    tdist.init_process_group(backend, **kw)
+    return True
+
+
+def barrier():
+    if tdist.is_available() and tdist.is_initialized():
+        tdist.barrier()
+
+
+def max_over_ranks(x, device=None):
+    """Max of a float over all ranks (the job ends when its slowest rank does)."""
+    if not (tdist.is_available() and tdist.is_initialized()):
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed_steps(step, steps, warmup, sync, device=None):
+    """Run `warmup` untimed steps, then time exactly `steps` steps between barrier + sync on
+    both sides; returns the max wall time over ranks (seconds)."""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    t1 = time.perf_counter()
+    barrier()
+    return max_over_ranks(t1 - t0, device)
+
+
+def whole_job_rate(bytes_per_rank, steps, wall, world):
+    """Aggregate GiB/s: every rank processes bytes_per_rank per step (weak scaling)."""
+    return world * bytes_per_rank * steps / wall / 2**30
+
+
+def close():
+    if tdist.is_available() and tdist.is_initialized():
+        barrier()
+        tdist.destroy_process_group()

@@ -40,9 +40,12 @@ def make_keys(n_keys, suites, seed=SEEDS["keys"], key_lens=None):
     return keys
 
 
-def tls_batch(n, lens, suites_per_key, n_keys=4096, content_type=23, seq_base=0):
-    """n TLS-mode records; lens: int or array (content lengths); record i uses slot i % n_keys."""
-    n_keys = min(n_keys, n) if n else 1
+def tls_batch(n, lens, suites_per_key, n_keys=4096, content_type=23, seq_base=0, first=0, shrink_keys=True):
+    """n TLS-mode records; lens: int or array (content lengths). The records are entries
+    first .. first+n-1 of a record stream in which entry g uses slot g % n_keys with sequence
+    number seq_base + g // n_keys (a shard of a larger batch when first > 0)."""
+    if shrink_keys:  # small ad-hoc batches: no more key slots than records
+        n_keys = min(n_keys, first + n) if n else 1
     lens = np.broadcast_to(np.asarray(lens, dtype=np.uint64), (n,)).copy()
     recs = np.zeros(n, dtype=REC_DTYPE)
     in_sz = _round16(lens)
@@ -50,9 +53,9 @@ def tls_batch(n, lens, suites_per_key, n_keys=4096, content_type=23, seq_base=0)
     recs["in_off"] = np.concatenate([[0], np.cumsum(in_sz)[:-1]]).astype(np.uint64) if n else []
     recs["out_off"] = np.concatenate([[0], np.cumsum(out_sz)[:-1]]).astype(np.uint64) if n else []
     recs["len"] = lens.astype(np.uint32)
-    slots = np.arange(n, dtype=np.uint64) % np.uint64(n_keys)
-    recs["key_slot"] = slots.astype(np.uint32)
-    recs["seq"] = seq_base + np.arange(n, dtype=np.uint64) // np.uint64(n_keys)
+    g = np.arange(first, first + n, dtype=np.uint64)
+    recs["key_slot"] = (g % np.uint64(n_keys)).astype(np.uint32)
+    recs["seq"] = seq_base + g // np.uint64(n_keys)
     recs["content_type"] = content_type
     recs["mode"] = MODE_TLS
     keys = make_keys(n_keys, suites_per_key(n_keys) if callable(suites_per_key) else
@@ -61,19 +64,36 @@ def tls_batch(n, lens, suites_per_key, n_keys=4096, content_type=23, seq_base=0)
                 out_bytes=int(out_sz.sum()) if n else 0, payload=int(lens.sum() + n))
 
 
-def config_batch(name, n=None):
-    """Descriptors for a BASELINE config (optionally the first n records of it)."""
+def config_batch(name, n=None, first=0):
+    """Descriptors for a BASELINE config: records first .. first+n-1 of it (default: all)."""
     suite, n_full, lens = CONFIGS[name]
-    n = n_full if n is None else n
+    n = n_full - first if n is None else n
     if suite == "mixed":
         rng = np.random.default_rng(SEEDS["layout"])
         lo, hi = lens
-        L = rng.integers(lo, hi + 1, size=n_full, dtype=np.uint64)[:n]
+        L = rng.integers(lo, hi + 1, size=max(n_full, first + n), dtype=np.uint64)[first:first + n]
 
         def suites(k):
             r = np.random.default_rng(SEEDS["layout"] + 1)
             return np.where(r.random(k) < 0.5, int(CipherSuite.TLS_AES_128_GCM_SHA256),
                             int(CipherSuite.TLS_CHACHA20_POLY1305_SHA256)).astype(np.uint16)
 
-        return tls_batch(n, L, suites)
-    return tls_batch(n, lens, int(suite))
+        return tls_batch(n, L, suites, n_keys=min(4096, n_full), first=first, shrink_keys=False)
+    return tls_batch(n, lens, int(suite), n_keys=min(4096, n_full), first=first, shrink_keys=False)
+
+
+# Configs BASELINE.json quotes on 8 GPUs: their records are split evenly over 8 ranks, and a rank
+# keeps that share whatever the GPU count (weak scaling). The others run whole on every GPU.
+EIGHT_GPU_CONFIGS = ("c4_aes256gcm_1Mi_x_16KiB", "c5_mixed_256Ki_x_64B-16KiB")
+
+
+def records_per_rank(name):
+    n_full = CONFIGS[name][1]
+    return n_full // 8 if name in EIGHT_GPU_CONFIGS else n_full
+
+
+def shard_batch(name, rank, n=None):
+    """Rank `rank`'s shard: records rank*n .. rank*n+n-1 of the config's record stream (key slots,
+    sequence numbers and lengths as in the unsharded batch). n defaults to records_per_rank()."""
+    n = records_per_rank(name) if n is None else n
+    return config_batch(name, n=n, first=rank * n)

@@ -27,6 +27,8 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+from anothertls_amd import dist  # noqa: E402
+
 METRIC = "GiB/s device-resident TLS-record AEAD (16 KiB recs); % HBM roofline @1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 
@@ -69,22 +71,16 @@ def cpu_baseline(batch, inbuf_host, budget_s):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as tdist
-
-        torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    rank, local, world = dist.env_ranks()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    dist.init("nccl", dev)
 
     import anothertls_amd as atls
     from anothertls_amd import workload
 
-    batch = workload.config_batch(args.config, n=args.records)
+    # this rank's shard of the config's record stream (weak scaling: fixed records per GPU)
+    batch = workload.shard_batch(args.config, rank, n=args.records)
     recs = batch["recs"]
     n = len(recs)
     eng = atls.Engine(local)
@@ -102,33 +98,27 @@ def main():
     def step():
         eng.seal_batch(d_recs.data_ptr(), d_in, d_aux, d_out, d_tags, flags=flags, n=n)
 
-    for _ in range(args.warmup):
-        step()
-    eng.sync()
+    def sync():
+        eng.sync()
+        torch.cuda.synchronize(dev)
 
+    # kernel time of the same steps from HIP events on the engine's stream
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if dist:
-        tdist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
+    marks = {"n": 0}
+
+    def timed_step():
+        if marks["n"] == args.warmup:
+            ev0.record(stream)
         step()
-    ev1.record(stream)
-    eng.sync()
-    torch.cuda.synchronize(dev)
-    t1 = time.perf_counter()
-    if dist:
-        tdist.barrier()
-    wall = t1 - t0
+        marks["n"] += 1
+        if marks["n"] == args.warmup + args.steps:
+            ev1.record(stream)
+
+    wall = dist.timed_steps(timed_step, args.steps, args.warmup, sync, dev)
     kern_ms = ev0.elapsed_time(ev1) / args.steps
-    if dist:
-        tt = torch.tensor([wall], dtype=torch.float64, device=dev)
-        tdist.all_reduce(tt, op=tdist.ReduceOp.MAX)
-        wall = float(tt.item())
 
     payload = batch["payload"]  # sum of AEAD lengths (content + type byte)
-    value = world * payload * args.steps / wall / 2**30
+    value = dist.whole_job_rate(payload, args.steps, wall, world)
     alg_bytes = 2 * payload + 16 * n
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
@@ -177,9 +167,7 @@ def main():
             result["pcie_inclusive_GiBps"] = round(3 * payload / (time.perf_counter() - t0) / 2**30, 3)
         print(json.dumps(result), flush=True)
     eng.close()
-    if dist:
-        tdist.barrier()
-        tdist.destroy_process_group()
+    dist.close()
 
 
 if __name__ == "__main__":

@@ -3,7 +3,8 @@
 The batch split (gcm_common.h bs_class/bs_taken) sends records of >= 1023 full blocks with a
 96-bit nonce to the bitsliced kernels and everything else to the T-table kernel. These tests
 build batches around that boundary and compare every byte and tag against the oracle, and the
-bitsliced engine against one with the bitsliced path switched off (ATLS_GCM_BS=0)."""
+bitsliced engine (ATLS_GCM_BS=1; off by default while it is slower than the T-table kernel on
+the headline config) against one with the bitsliced path switched off (ATLS_GCM_BS=0)."""
 import os
 
 import numpy as np

@@ -28,6 +28,8 @@ for step in "$@"; do
     bench_c4) run bench_c4 600 python bench.py --config c4_aes256gcm_1Mi_x_16KiB --records 65536 --no-cpu-baseline ;;
     pmc_bs) export TMPDIR=/tmp; run pmc_bs1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_bs1 -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline && \
             run pmc_bs2 600 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS -d gpurun_out/pmc_bs2 -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    stamps) run stamps 300 python tools/bs_stamps.py ;;
+    bs_debug) run bs_debug 120 python tools/bs_debug.py ;;
     bench_c3) run bench_c3 600 python bench.py --config c3_chacha20poly1305_64Ki_x_1.5KiB --no-cpu-baseline ;;
     bench_c5) run bench_c5 600 python bench.py --config c5_mixed_256Ki_x_64B-16KiB --no-cpu-baseline ;;
     prof) export TMPDIR=/tmp; run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
