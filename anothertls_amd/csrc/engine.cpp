@@ -25,7 +25,7 @@ extern "C" int atls_launch_key_setup(const atls_key* keys, uint32_t n, void* ks,
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
-                               int bs_on, int grid, hipStream_t s);
+                               int bs_on, int nr_mask, int grid, hipStream_t s);
 extern "C" int atls_launch_gcm_bs(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
@@ -157,7 +157,8 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   if (rc) return rc;
   if (e->has_aes)
     rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
-                         (const uint32_t*)e->t0.p, (uint32_t*)e->err.p, e->n_slots, bs ? 1 : 0, e->cus * 2, s);
+                         (const uint32_t*)e->t0.p, (uint32_t*)e->err.p, e->n_slots, bs ? 1 : 0, e->aes_nr_mask,
+                         e->cus * 2, s);
   if (rc) return rc;
   if (e->has_chacha)
     rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,

@@ -108,7 +108,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   uint32_t rk[4 * (NR + 1)], rkr[4 * (NR + 1)];
 #pragma unroll
   for (int i = 0; i < 4 * (NR + 1); i++) {
-    rk[i] = k->rk[i];
+    rk[i] = cptr(k->rk)[i];  // wave-uniform: scalar loads into SGPRs
     rkr[i] = rot16(rk[i]);
   }
 
@@ -358,8 +358,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 
 // WAVES waves per workgroup (one record per wave at a time), one workgroup per CU: the LDS
 // footprint (64 KiB tables + 8 KiB per wave) is what limits residency.
-template <bool OPEN, int kWaves>
-__global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
+// One launch per AES round count present in the key table (a kernel holds only that count's
+// round keys, in SGPRs); the launch with `report` set also reports the records no launch takes.
+template <bool OPEN, int kWaves, int NR>
+__global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A, uint32_t report) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
     const uint32_t v = A.t0[i >> (kNTab == 2 ? 6 : 5)];
@@ -376,50 +378,40 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
     d.key_slot = uni(d.key_slot);
     d.len = uni(d.len);
     d.mode = (uint8_t)uni(d.mode);
+    uint32_t status = 0;  // != 0: this record fails with that status (reported by one launch)
+    const KeySched* k = A.ks + (d.key_slot < A.n_slots ? d.key_slot : 0u);
     if (d.key_slot >= A.n_slots || d.mode > ATLS_MODE_RAW) {
-      if (lane == 0) {
+      status = ATLS_ILLEGAL_PARAMETER;
+    } else {
+      const uint32_t suite = uni(k->suite);
+      if (suite == kSuiteChacha) continue;  // ChaCha20-Poly1305 records: chacha.hip
+      if (suite != kSuiteAes128 && suite != kSuiteAes256) status = ATLS_INSUFFICIENT_SECURITY;  // get_cipher (:84)
+      else if (!uni(k->valid)) status = ATLS_ILLEGAL_PARAMETER;
+    }
+    if (status) {
+      if (report && lane == 0) {
         atomicOr(A.err, 1u);
         if (OPEN) {
-          atls_open_result rr = {0, ATLS_ILLEGAL_PARAMETER, 0, {0, 0}};
+          atls_open_result rr = {0, (uint8_t)status, 0, {0, 0}};
           A.res[r] = rr;
         }
       }
       continue;
     }
-    const KeySched* k = A.ks + d.key_slot;
-    const uint32_t suite = uni(k->suite);
-    if (suite == kSuiteChacha) continue;  // ChaCha20-Poly1305 records: chacha.hip
-    if (suite != kSuiteAes128 && suite != kSuiteAes256) {  // CipherSuite::get_cipher fails (:84)
-      if (lane == 0) {
-        atomicOr(A.err, 1u);
-        if (OPEN) {
-          atls_open_result rr = {0, ATLS_INSUFFICIENT_SECURITY, 0, {0, 0}};
-          A.res[r] = rr;
-        }
-      }
-      continue;
-    }
-    const uint32_t nr = uni(k->valid) ? uni(k->nr) : 0u;
-    if (nr == 10) gcm_record<10, OPEN>(A, d, k, r, lb, wb, lane);
-    else if (nr == 14) gcm_record<14, OPEN>(A, d, k, r, lb, wb, lane);
-    else if (nr == 12) gcm_record<12, OPEN>(A, d, k, r, lb, wb, lane);
-    else if (lane == 0) {
-      atomicOr(A.err, 1u);
-      if (OPEN) {
-        atls_open_result rr = {0, ATLS_ILLEGAL_PARAMETER, 0, {0, 0}};
-        A.res[r] = rr;
-      }
-    }
+    if (uni(k->nr) != (uint32_t)NR) continue;  // another launch's round count
+    gcm_record<NR, OPEN>(A, d, k, r, lb, wb, lane);
     wave_lds_sync();  // table reads of this record done before the next record rebuilds it
   }
 }
 
 }  // namespace atls
 
+// nr_mask: bit 0/1/2 = key slots with 10/12/14 rounds exist (one launch each; with none, one
+// launch still reports the invalid records).
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
-                               int bs_on, int grid, hipStream_t s) {
+                               int bs_on, int nr_mask, int grid, hipStream_t s) {
   if (n == 0) return 0;
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, err, n_slots,
                   (uint32_t)(bs_on != 0)};
@@ -432,13 +424,21 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
   const dim3 block(64 * waves);
   const size_t lds = atls::lds_bytes(waves);
-#define ATLS_LAUNCH(W)                                                                        \
-  if (waves == W) {                                                                           \
-    if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W>), dim3(g), block, lds, s, A);     \
-    else hipLaunchKernelGGL((atls::gcm_kernel<false, W>), dim3(g), block, lds, s, A);         \
+  if ((nr_mask & 7) == 0) nr_mask = 1;
+  uint32_t report = 1;
+#define ATLS_LAUNCH_NR(W, NR)                                                                           \
+  if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR>), dim3(g), block, lds, s, A, report);     \
+  else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR>), dim3(g), block, lds, s, A, report);         \
+  report = 0;
+#define ATLS_LAUNCH(W)                                 \
+  if (waves == W) {                                    \
+    if (nr_mask & 1) { ATLS_LAUNCH_NR(W, 10) }         \
+    if (nr_mask & 2) { ATLS_LAUNCH_NR(W, 12) }         \
+    if (nr_mask & 4) { ATLS_LAUNCH_NR(W, 14) }         \
   }
   ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(12)
   if constexpr (atls::kNTab == 1) { ATLS_LAUNCH(16) }
 #undef ATLS_LAUNCH
+#undef ATLS_LAUNCH_NR
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }

@@ -23,7 +23,7 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     bench_waves) for w in 4 8 12; do ATLS_GCM_WAVES=$w run bench_w$w 300 python bench.py --no-cpu-baseline; done ;;
     pmc_lds) export TMPDIR=/tmp; run pmc_lds 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmc_lds -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
-    variants) for lib in anothertls_amd/variants/libatls_*.so; do for w in 8 12 16; do t=$(basename $lib .so)_w$w; ATLS_LIB=$PWD/$lib ATLS_GCM_WAVES=$w run var_$t 300 python bench.py --no-cpu-baseline --steps 10; done; done ;;
+    variants) for lib in anothertls_amd/variants/libatls_nb*.so; do for w in 8 12 16; do t=$(basename $lib .so)_w$w; ATLS_LIB=$PWD/$lib ATLS_GCM_WAVES=$w run var_$t 300 python bench.py --no-cpu-baseline --steps 10; done; done ;;
     bench_tt) ATLS_GCM_BS=0 run bench_tt 300 python bench.py --no-cpu-baseline --steps 10 ;;
     bench_c4) run bench_c4 600 python bench.py --config c4_aes256gcm_1Mi_x_16KiB --records 65536 --no-cpu-baseline ;;
     pmc_bs) export TMPDIR=/tmp; run pmc_bs1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE -d gpurun_out/pmc_bs1 -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline && \
