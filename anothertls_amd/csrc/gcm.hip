@@ -25,93 +25,163 @@
 
 namespace atls {
 
-#ifndef ATLS_GCM_NB
-#define ATLS_GCM_NB 1
+#ifndef ATLS_GHASH_W
+#define ATLS_GHASH_W 0  // > 0: GHASH lookups issued per LDS round trip (ghash_mul_tab_wide); 0: compiler schedule
 #endif
-#ifndef ATLS_GCM_NTAB
-#define ATLS_GCM_NTAB 2
+#ifndef ATLS_CTR_CACHE
+#define ATLS_CTR_CACHE 1
 #endif
-constexpr int kNB = ATLS_GCM_NB;      // independent AES blocks per lane per step (ILP)
-constexpr int kNTab = ATLS_GCM_NTAB;  // replicated T-tables in LDS (2: T0,T1; 1: T0 + rotates)
-// LDS: AES tables first. kNTab = 2: row x = 256 B = {T0[x] x32 banks | T1[x] x32 banks} (64 KiB);
-// kNTab = 1: row x = 128 B = T0[x] x32 banks (32 KiB). Then one 8 KiB GHASH table per wave.
+// LDS: AES tables first, row x = 256 B = {T0[x] x32 banks | T1[x] x32 banks} (64 KiB), then one
+// 8 KiB GHASH table per wave.
 // Lane l reads bank (l & 31): conflict-free ds_read_b32.
-constexpr int kTabBytes = kNTab == 2 ? 65536 : 32768;
+constexpr int kTabBytes = 65536;
 constexpr int kGhashBytes = 8192;
 constexpr size_t lds_bytes(int waves) { return kTabBytes + (size_t)waves * kGhashBytes; }
+
+template <int W>
+__device__ __forceinline__ void ghash_mul(uint32_t (&y)[4], uint32_t wb) {
+  if constexpr (W == 0) ghash_mul_tab(y, wb);
+  else ghash_mul_tab_wide<W>(y, wb);
+}
+
+// Round-key words from the key schedule: a wave-uniform address, so one s_load_dwordx4.
+__device__ __forceinline__ v4u32 kload4(const uint32_t* p) {
+  return *(const __attribute__((address_space(4))) v4u32*)(p);
+}
 
 // ---- AES (two-table T-table rounds on raw-word state) -------------------------------------
 // T0[x] = {2S,S,S,3S} (LE), T1 = rotl8(T0). With T2 = rotl16(T0), T3 = rotl16(T1):
 //   col_c = T0[s_c.b0] ^ T1[s_{c+1}.b1] ^ rotl16(T0[s_{c+2}.b2] ^ T1[s_{c+3}.b3] ^ rotl16(rk_c)).
 // Table address of byte k of state word w for this lane's bank: (byte << 8) | lb, one v_perm_b32
 // (selector byte 0 <- lb, byte 1 <- w.byte_k, bytes 2-3 <- 0); lb = 4*(lane & 31); T1 at +128.
-#define TA(w, sh) (kNTab == 2 ? perm((w), lb, 0x0c0c0000u | ((4u + (sh) / 8u) << 8)) \
-                              : ((((w) >> (sh)) & 0xffu) << 7 | lb))
-template <int NR, int NB>
-__device__ __forceinline__ void aes_encrypt_tt(uint32_t (&s)[NB][4], const uint32_t* rk, const uint32_t* rkr,
-                                               uint32_t lb) {
+#define TA(w, sh) perm((w), lb, 0x0c0c0000u | ((4u + (sh) / 8u) << 8))
+
+// One middle round; kr = rotl16 of the round key words. The compiler's own interleaving of
+// lookups and XORs measured faster than issuing all 16 lookups first (tools/ubench/step_ubench).
+__device__ __forceinline__ void tt_round(uint32_t (&s)[4], const uint32_t* kr, uint32_t lb) {
+  const uint32_t s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
 #pragma unroll
-  for (int b = 0; b < NB; b++) {
-#pragma unroll
-    for (int i = 0; i < 4; i++) s[b][i] ^= rk[i];
-  }
-#pragma unroll
-  for (int r = 1; r < NR; r++) {
-#pragma unroll
-    for (int b = 0; b < NB; b++) {
-      const uint32_t s0 = s[b][0], s1 = s[b][1], s2 = s[b][2], s3 = s[b][3];
-      uint32_t t[4];
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const uint32_t a = (c == 0 ? s0 : c == 1 ? s1 : c == 2 ? s2 : s3);
-        const uint32_t bb = (c == 0 ? s1 : c == 1 ? s2 : c == 2 ? s3 : s0);
-        const uint32_t cc = (c == 0 ? s2 : c == 1 ? s3 : c == 2 ? s0 : s1);
-        const uint32_t dd = (c == 0 ? s3 : c == 1 ? s0 : c == 2 ? s1 : s2);
-        if (kNTab == 2) {
-          const uint32_t u = xor3(lds_u32(TA(cc, 16)), lds_u32(TA(dd, 24) + 128), rkr[4 * r + c]);
-          t[c] = xor3(lds_u32(TA(a, 0)), lds_u32(TA(bb, 8) + 128), rot16(u));
-        } else {
-          const uint32_t u = xor3(lds_u32(TA(cc, 16)), rotl32(lds_u32(TA(dd, 24)), 8), rkr[4 * r + c]);
-          t[c] = xor3(lds_u32(TA(a, 0)), rotl32(lds_u32(TA(bb, 8)), 8), rot16(u));
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 4; c++) s[b][c] = t[c];
-    }
-  }
-  // Final round (SubBytes, ShiftRows, AddRoundKey): S[x] = byte 1 of T0[x] = byte 2, 3 of T1[x].
-#pragma unroll
-  for (int b = 0; b < NB; b++) {
-    const uint32_t s0 = s[b][0], s1 = s[b][1], s2 = s[b][2], s3 = s[b][3];
-    uint32_t t[4];
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const uint32_t a = (c == 0 ? s0 : c == 1 ? s1 : c == 2 ? s2 : s3);
-      const uint32_t bb = (c == 0 ? s1 : c == 1 ? s2 : c == 2 ? s3 : s0);
-      const uint32_t cc = (c == 0 ? s2 : c == 1 ? s3 : c == 2 ? s0 : s1);
-      const uint32_t dd = (c == 0 ? s3 : c == 1 ? s0 : c == 2 ? s1 : s2);
-      // {T0[a].b1, T0[b].b1} | {T1[c].b2, T1[d].b3}, then ^ rk: two v_perm + one v_bitop3 ((x|y)^z)
-      const uint32_t lo = perm(lds_u32(TA(bb, 8)), lds_u32(TA(a, 0)), 0x0c0c0501u);
-      const uint32_t hi = kNTab == 2 ? perm(lds_u32(TA(dd, 24) + 128), lds_u32(TA(cc, 16) + 128), 0x07020c0cu)
-                                     : perm(lds_u32(TA(dd, 24)), lds_u32(TA(cc, 16)), 0x05010c0cu);
-      t[c] = __builtin_amdgcn_bitop3_b32(lo, hi, rk[4 * NR + c], 0x56);
-    }
-#pragma unroll
-    for (int c = 0; c < 4; c++) s[b][c] = t[c];
+  for (int c = 0; c < 4; c++) {
+    const uint32_t a = (c == 0 ? s0 : c == 1 ? s1 : c == 2 ? s2 : s3);
+    const uint32_t bb = (c == 0 ? s1 : c == 1 ? s2 : c == 2 ? s3 : s0);
+    const uint32_t cc = (c == 0 ? s2 : c == 1 ? s3 : c == 2 ? s0 : s1);
+    const uint32_t dd = (c == 0 ? s3 : c == 1 ? s0 : c == 2 ? s1 : s2);
+    const uint32_t u = xor3(lds_u32(TA(cc, 16)), lds_u32(TA(dd, 24) + 128), kr[c]);
+    s[c] = xor3(lds_u32(TA(a, 0)), lds_u32(TA(bb, 8) + 128), rot16(u));
   }
 }
+
+// Final round (SubBytes, ShiftRows, AddRoundKey): S[x] = byte 1 of T0[x] = byte 2, 3 of T1[x].
+__device__ __forceinline__ void tt_final(uint32_t (&s)[4], const uint32_t* kf, uint32_t lb) {
+  const uint32_t s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t a = (c == 0 ? s0 : c == 1 ? s1 : c == 2 ? s2 : s3);
+    const uint32_t bb = (c == 0 ? s1 : c == 1 ? s2 : c == 2 ? s3 : s0);
+    const uint32_t cc = (c == 0 ? s2 : c == 1 ? s3 : c == 2 ? s0 : s1);
+    const uint32_t dd = (c == 0 ? s3 : c == 1 ? s0 : c == 2 ? s1 : s2);
+    // {T0[a].b1, T0[b].b1} | {T1[c].b2, T1[d].b3}, then ^ rk: two v_perm + one v_bitop3 ((x|y)^z)
+    const uint32_t lo = perm(lds_u32(TA(bb, 8)), lds_u32(TA(a, 0)), 0x0c0c0501u);
+    const uint32_t hi = perm(lds_u32(TA(dd, 24) + 128), lds_u32(TA(cc, 16) + 128), 0x07020c0cu);
+    s[c] = __builtin_amdgcn_bitop3_b32(lo, hi, kf[c], 0x56);
+  }
+}
+
+// Rounds R0 .. NR on a state that went through rounds 0 .. R0-1. rk / rkr: the record's round
+// keys and their rotl16, held in (wave-uniform) registers for the whole record -- measured
+// faster than a rolled round loop with a scalar load per round.
+template <int NR, int R0>
+__device__ __forceinline__ void aes_rounds_tt(uint32_t (&s)[4], const uint32_t* rk, const uint32_t* rkr,
+                                              uint32_t lb) {
+#pragma unroll
+  for (int r = R0; r < NR; r++) tt_round(s, rkr + 4 * r, lb);
+  tt_final(s, rk + 4 * NR, lb);
+}
+
+template <int NR>
+__device__ __forceinline__ void aes_encrypt_tt(uint32_t (&s)[4], const uint32_t* rk, const uint32_t* rkr,
+                                               uint32_t lb) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) s[i] ^= rk[i];
+  aes_rounds_tt<NR, 1>(s, rk, rkr, lb);
+}
+
+// ---- counter-mode caching (Bernstein & Schwabe, "New AES software speed records", 2008) ----
+// In one 64-slot step the counters are ctr = 256*hi + lo with hi wave-uniform, so the 64 counter
+// blocks differ only in byte 15. Round 1 then has ONE lane-varying lookup (byte 15 -> T3 into
+// column 0) and round 2 FOUR (column 0 of the round-1 state feeds one byte of each column); the
+// other 27 lookups and round-key XORs fold into five words that depend on (record, hi) only:
+//   c0   = T3[lo ^ rk0.b15] ^ U0            (round-1 column 0; columns 1-3 are V1..V3)
+//   out0 = T0[c0.b0] ^ K0,  K0 = T1[V1.b1] ^ T2[V2.b2] ^ T3[V3.b3] ^ rk2_0
+//   out1 = T3[c0.b3] ^ K1,  K1 = T0[V1.b0] ^ T1[V2.b1] ^ T2[V3.b2] ^ rk2_1
+//   out2 = T2[c0.b2] ^ K2,  K2 = T0[V2.b0] ^ T1[V3.b1] ^ T3[V1.b3] ^ rk2_2
+//   out3 = T1[c0.b1] ^ K3,  K3 = T0[V3.b0] ^ T2[V1.b2] ^ T3[V2.b3] ^ rk2_3
+// AES-128 does 133 lookups per block instead of 160. Lane j of the wave holds the five words for
+// hi = hi0 + j (built once per record); a step reads its hi's words with v_readlane.
+struct CtrCache {
+  uint32_t u0r, k0, k1r, k2r, k3;  // u0r = rot16(U0), k1r = rot16(K1), k2r = rot16(K2)
+};
+
+// nraw: nonce bytes 0..11 as raw words; hi: this lane's counter high part (ctr >> 8).
+__device__ __forceinline__ CtrCache ctr_cache_build(const uint32_t (&nraw)[3], uint32_t hi, const uint32_t* rk,
+                                                    const uint32_t* rkr, uint32_t lb) {
+  const uint32_t s0 = nraw[0] ^ rk[0], s1 = nraw[1] ^ rk[1], s2 = nraw[2] ^ rk[2];
+  const uint32_t s3 = bswap32(hi << 8) ^ rk[3];  // lo = 0: byte 15 never enters U0 / V1..V3
+  const uint32_t u0 = xor3(lds_u32(TA(s0, 0)), lds_u32(TA(s1, 8) + 128), rot16(lds_u32(TA(s2, 16)) ^ rkr[4]));
+  const uint32_t* kr1 = rkr + 4;
+  uint32_t v[4];
+#pragma unroll
+  for (int c = 1; c < 4; c++) {
+    const uint32_t a = (c == 1 ? s1 : c == 2 ? s2 : s3), bb = (c == 1 ? s2 : c == 2 ? s3 : s0);
+    const uint32_t cc = (c == 1 ? s3 : c == 2 ? s0 : s1), dd = (c == 1 ? s0 : c == 2 ? s1 : s2);
+    const uint32_t u = xor3(lds_u32(TA(cc, 16)), lds_u32(TA(dd, 24) + 128), kr1[c]);
+    v[c] = xor3(lds_u32(TA(a, 0)), lds_u32(TA(bb, 8) + 128), rot16(u));
+  }
+  CtrCache C;
+  C.u0r = rot16(u0);
+  // T2[x] = rot16(T0[x]), T3[x] = rot16(T1[x])
+  C.k0 = xor3(lds_u32(TA(v[1], 8) + 128), rot16(lds_u32(TA(v[2], 16)) ^ lds_u32(TA(v[3], 24) + 128)), rk[8]);
+  C.k1r = rot16(xor3(lds_u32(TA(v[1], 0)), lds_u32(TA(v[2], 8) + 128), rot16(lds_u32(TA(v[3], 16))) ^ rk[9]));
+  C.k2r = rot16(xor3(lds_u32(TA(v[2], 0)), lds_u32(TA(v[3], 8) + 128), rot16(lds_u32(TA(v[1], 24) + 128)) ^ rk[10]));
+  C.k3 = xor3(lds_u32(TA(v[3], 0)), rot16(lds_u32(TA(v[1], 16)) ^ lds_u32(TA(v[2], 24) + 128)), rk[11]);
+  return C;
+}
+
+// Rounds 1 and 2 of one lane's counter block from the cache; addr1 = T0 address of
+// lo ^ rk0.b15 for this lane's bank. Leaves the state after round 2.
+__device__ __forceinline__ void aes_ctr_r12(uint32_t (&s)[4], uint32_t addr1, const CtrCache& C, uint32_t lb) {
+  const uint32_t c0r = lds_u32(addr1 + 128) ^ C.u0r;  // rot16 of round-1 column 0
+  // bytes of c0 = rot16(c0r): c0.b0 = c0r.b2, c0.b1 = c0r.b3, c0.b2 = c0r.b0, c0.b3 = c0r.b1
+  s[0] = lds_u32(TA(c0r, 16)) ^ C.k0;
+  s[1] = rot16(lds_u32(TA(c0r, 8) + 128) ^ C.k1r);
+  s[2] = rot16(lds_u32(TA(c0r, 0)) ^ C.k2r);
+  s[3] = lds_u32(TA(c0r, 24) + 128) ^ C.k3;
+}
 #undef TA
+
+// Phase timing (build with -DATLS_TT_STAMPS): shader-clock totals over all records, read back with
+// atls_debug_tt_stamps(). 0 setup (tables, counter cache), 1 fast steps, 2 general steps,
+// 3 lane combine + tag, 4 records, 5 fast steps, 6 general steps.
+#ifdef ATLS_TT_STAMPS
+__device__ unsigned long long g_tt_stamps[8];
+#define TT_STAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
+#else
+#define TT_STAMP(var)
+#endif
 
 template <int NR, bool OPEN>
 __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx,
                            uint32_t lb, uint32_t wb, int lane) {
+  TT_STAMP(t_start);
+#ifdef ATLS_TT_STAMPS
+  uint64_t t_fast = 0, t_gen = 0, n_fast = 0, n_gen = 0;
+#endif
   uint32_t rk[4 * (NR + 1)], rkr[4 * (NR + 1)];
 #pragma unroll
   for (int i = 0; i < 4 * (NR + 1); i++) {
-    rk[i] = cptr(k->rk)[i];  // wave-uniform: scalar loads into SGPRs
-    rkr[i] = rot16(rk[i]);
+    rk[i] = cptr(k->rk)[i];  // wave-uniform: scalar loads
+    rkr[i] = cptr(k->rkr)[i];
   }
-
   const bool tls = d.mode == ATLS_MODE_TLS;
   const uint32_t len = d.len;
   const uint32_t n_aead = (tls && !OPEN) ? len + 1 : len;  // record.rs:172-173 inner plaintext
@@ -183,87 +253,106 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0), lane 0
   int64_t lastnz = -1;                      // OPEN+TLS: (pos << 8 | byte) of last non-zero pt byte
   const bool fast_src = src_al, fast_dst = dst_al;
-  // Slots [64*kNB, fast_end) are full 16-byte data blocks that lie wholly inside the input and
+  // Slots [64, fast_end) are full 16-byte data blocks that lie wholly inside the input and
   // output: for them the step below runs branch-free (no classification, no partial handling).
   const uint32_t full_blocks = min(in_bytes, n_aead) / 16u;
   const uint32_t fast_end = (src_al && dst_al && is96) ? na + 1u + full_blocks : 0u;
 
-  for (uint32_t base = 0; base < S; base += 64 * kNB) {
-    if (base >= 64u * kNB && base + 64u * kNB <= fast_end) {  // wave-uniform
-      uint32_t st[kNB][4];
-      v4u32 P[kNB];
-#pragma unroll
-      for (int b = 0; b < kNB; b++) {
-        const uint32_t s = base + 64u * b + (uint32_t)lane;
-        const uint32_t off = (s - 1u - na) * 16u;
-        P[b] = *reinterpret_cast<const v4u32*>(src + off);
-        st[b][0] = bswap32(j0[0]); st[b][1] = bswap32(j0[1]); st[b][2] = bswap32(j0[2]);
-        st[b][3] = bswap32(j0[3] + (s - na));
+  // Counter cache (CtrCache): every 64-slot step's counters share ctr >> 8 when the counter of slot
+  // `base` is a multiple of 64 -- records with one AAD block (all TLS records) and a 96-bit IV.
+  // Lane j holds the words of hi = j, enough for records below 2^14 blocks (256 KiB).
+  const bool use_cache = ATLS_CTR_CACHE && is96 && na == 1u && S <= 64u * 256u;
+  const uint32_t nraw[3] = {bswap32(j0[0]), bswap32(j0[1]), bswap32(j0[2])};
+  const uint32_t lane_addr = ((uint32_t)lane << 8) | lb;  // T0 address of byte value `lane`
+  const uint32_t k15 = rk[3] >> 24;                       // rk0 byte 15
+  CtrCache cc{};
+  if (use_cache) cc = ctr_cache_build(nraw, (uint32_t)lane, rk, rkr, lb);
+  // AES of this lane's counter block via the cache; j = the step's (wave-uniform) ctr >> 8.
+  auto aes_cached = [&](uint32_t (&st4)[4], uint32_t addr1, uint32_t j) {
+    const CtrCache cj{(uint32_t)__builtin_amdgcn_readlane((int)cc.u0r, (int)j),
+                      (uint32_t)__builtin_amdgcn_readlane((int)cc.k0, (int)j),
+                      (uint32_t)__builtin_amdgcn_readlane((int)cc.k1r, (int)j),
+                      (uint32_t)__builtin_amdgcn_readlane((int)cc.k2r, (int)j),
+                      (uint32_t)__builtin_amdgcn_readlane((int)cc.k3, (int)j)};
+    aes_ctr_r12(st4, addr1, cj, lb);
+    aes_rounds_tt<NR, 3>(st4, rk, rkr, lb);
+  };
+
+  TT_STAMP(t_setup);
+  for (uint32_t base = 0; base < S; base += 64) {
+    TT_STAMP(t_step);
+    const uint32_t s = base + (uint32_t)lane;
+    if (base >= 64u && base + 64u <= fast_end) {  // wave-uniform
+      const uint32_t off = (s - 1u - na) * 16u;
+      const v4u32 P = *reinterpret_cast<const v4u32*>(src + off);
+      uint32_t st[4];
+      if (use_cache) {
+        const uint32_t c0 = j0[3] + base - na;  // counter of lane 0, a multiple of 64
+        aes_cached(st, lane_addr ^ (((c0 & 0xffu) ^ k15) << 8), c0 >> 8);
+      } else {
+        st[0] = nraw[0]; st[1] = nraw[1]; st[2] = nraw[2];
+        st[3] = bswap32(j0[3] + (s - na));
+        aes_encrypt_tt<NR>(st, rk, rkr, lb);
       }
-      aes_encrypt_tt<NR, kNB>(st, rk, rkr, lb);
-#pragma unroll
-      for (int b = 0; b < kNB; b++) {
-        const uint32_t s = base + 64u * b + (uint32_t)lane;
-        const uint32_t off = (s - 1u - na) * 16u;
-        const v4u32 C = {P[b].x ^ st[b][0], P[b].y ^ st[b][1], P[b].z ^ st[b][2], P[b].w ^ st[b][3]};
-        *reinterpret_cast<v4u32*>(dst + off) = C;
-        const v4u32 Bv = OPEN ? P[b] : C;
-        if (OPEN && tls) {
-          const uint32_t cw[4] = {C.x, C.y, C.z, C.w};
-          const int j = last_nonzero(cw, 16);
-          if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((cw[j >> 2] >> (8 * (j & 3))) & 0xffu);
-        }
-        ghash_mul_tab(y, wb);
-        y[0] ^= Bv.x; y[1] ^= Bv.y; y[2] ^= Bv.z; y[3] ^= Bv.w;
+      const v4u32 C = {P.x ^ st[0], P.y ^ st[1], P.z ^ st[2], P.w ^ st[3]};
+      *reinterpret_cast<v4u32*>(dst + off) = C;
+      const v4u32 Bv = OPEN ? P : C;
+      if (OPEN && tls) {
+        const uint32_t cw[4] = {C.x, C.y, C.z, C.w};
+        const int j = last_nonzero(cw, 16);
+        if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((cw[j >> 2] >> (8 * (j & 3))) & 0xffu);
       }
+      ghash_mul<ATLS_GHASH_W>(y, wb);
+      y[0] ^= Bv.x; y[1] ^= Bv.y; y[2] ^= Bv.z; y[3] ^= Bv.w;
+#ifdef ATLS_TT_STAMPS
+      t_fast += __builtin_amdgcn_s_memtime() - t_step;
+      n_fast++;
+#endif
       continue;
     }
-    uint32_t st[kNB][4];
-    uint32_t P[kNB][4];
+    // counter block J0 + c (gcm.rs:89-96): c = s - na for data block s - 1 - na, 0 for slots 0..na
+    const uint32_t c = (s > na) ? (s - na) : 0u;
+    uint32_t cb[4] = {j0[0], j0[1], j0[2], j0[3]};
+    if (is96) {
+      cb[3] = j0[3] + c;  // (Yi & !0xFFFFFFFF) | counter, counter mod 2^32
+    } else {            // Yi + counter as a 128-bit add
+      uint64_t lo = (((uint64_t)cb[2] << 32) | cb[3]) + c;
+      uint64_t hi = ((uint64_t)cb[0] << 32) | cb[1];
+      if (lo < c) hi++;
+      cb[0] = (uint32_t)(hi >> 32); cb[1] = (uint32_t)hi; cb[2] = (uint32_t)(lo >> 32); cb[3] = (uint32_t)lo;
+    }
+    uint32_t st[4];
 #pragma unroll
-    for (int b = 0; b < kNB; b++) {
-      const uint32_t s = base + 64u * b + (uint32_t)lane;
-      // counter block J0 + c (gcm.rs:89-96): c = b + 1 for data block b, 0 for slot 0
-      const uint32_t c = (s > na) ? (s - na) : 0u;
-      uint32_t cb[4] = {j0[0], j0[1], j0[2], j0[3]};
-      if (is96) {
-        cb[3] = j0[3] + c;  // (Yi & !0xFFFFFFFF) | counter, counter mod 2^32
-      } else {            // Yi + counter as a 128-bit add
-        uint64_t lo = (((uint64_t)cb[2] << 32) | cb[3]) + c;
-        uint64_t hi = ((uint64_t)cb[0] << 32) | cb[1];
-        if (lo < c) hi++;
-        cb[0] = (uint32_t)(hi >> 32); cb[1] = (uint32_t)hi; cb[2] = (uint32_t)(lo >> 32); cb[3] = (uint32_t)lo;
-      }
+    for (int w = 0; w < 4; w++) st[w] = bswap32(cb[w]);
+    // issue the data load before the AES rounds so HBM latency hides under them
+    uint32_t P[4] = {0, 0, 0, 0};
+    const uint32_t g = s - 1;
+    if (s >= 1 && s <= m && g >= na && g < na + nb) {
+      const uint32_t off = (g - na) * 16;
+      if (off + 16 <= in_bytes && fast_src) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src + off);
+        P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
+      } else {
+        const uint32_t valid = min(16u, n_aead - off);
 #pragma unroll
-      for (int w = 0; w < 4; w++) st[b][w] = bswap32(cb[w]);
-      // issue the data load before the AES rounds so HBM latency hides under them
-      P[b][0] = P[b][1] = P[b][2] = P[b][3] = 0;
-      const uint32_t g = s - 1;
-      if (s >= 1 && s <= m && g >= na && g < na + nb) {
-        const uint32_t off = (g - na) * 16;
-        if (off + 16 <= in_bytes && fast_src) {
-          const uint4 v = *reinterpret_cast<const uint4*>(src + off);
-          P[b][0] = v.x; P[b][1] = v.y; P[b][2] = v.z; P[b][3] = v.w;
-        } else {
-          const uint32_t valid = min(16u, n_aead - off);
-#pragma unroll
-          for (int q = 0; q < 16; q++) {  // compile-time byte index keeps P in registers
-            if ((uint32_t)q < valid) {
-              const uint32_t byte = (off + q < in_bytes) ? src[off + q] : (uint32_t)d.content_type;  // record.rs:173
-              P[b][q >> 2] |= byte << (8 * (q & 3));
-            }
+        for (int q = 0; q < 16; q++) {  // compile-time byte index keeps P in registers
+          if ((uint32_t)q < valid) {
+            const uint32_t byte = (off + q < in_bytes) ? src[off + q] : (uint32_t)d.content_type;  // record.rs:173
+            P[q >> 2] |= byte << (8 * (q & 3));
           }
         }
       }
     }
-    aes_encrypt_tt<NR, kNB>(st, rk, rkr, lb);
-#pragma unroll
-    for (int b = 0; b < kNB; b++) {
-      const uint32_t s = base + 64u * b + (uint32_t)lane;
-      if (s == 0) { e0 = st[b][0]; e1 = st[b][1]; e2 = st[b][2]; e3 = st[b][3]; }
-      if (s == 0 || s > m) continue;
-      const uint32_t g = s - 1;
-      uint32_t B[4] = {0, 0, 0, 0};
+    if (use_cache) {  // ctr = 1 for slots 0..na, else 1 + s - na: the step's ctr >> 8 is lane 63's
+      const uint32_t ctr = cb[3];
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)ctr, 63) >> 8;
+      aes_cached(st, perm((ctr & 0xffu) ^ k15, lb, 0x0c0c0400u), hi);
+    } else {
+      aes_encrypt_tt<NR>(st, rk, rkr, lb);
+    }
+    if (s == 0) { e0 = st[0]; e1 = st[1]; e2 = st[2]; e3 = st[3]; }
+    uint32_t B[4] = {0, 0, 0, 0};
+    if (s >= 1 && s <= m) {
       if (g < na) {  // AAD block (gcm.rs:78-87), zero-padded at the end (bytes.rs:110-121)
         if (tls) {
           B[0] = hdr0; B[1] = hdr1;
@@ -276,7 +365,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       } else if (g < na + nb) {  // data block (gcm.rs:89-119)
         const uint32_t off = (g - na) * 16;
         const uint32_t valid = min(16u, n_aead - off);
-        uint32_t C[4] = {P[b][0] ^ st[b][0], P[b][1] ^ st[b][1], P[b][2] ^ st[b][2], P[b][3] ^ st[b][3]};
+        uint32_t C[4] = {P[0] ^ st[0], P[1] ^ st[1], P[2] ^ st[2], P[3] ^ st[3]};
         if (valid < 16) {  // (data ^ Ek) >> overflow: only `valid` bytes exist
 #pragma unroll
           for (int w = 0; w < 4; w++) {
@@ -293,7 +382,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
         }
         if (OPEN) {
 #pragma unroll
-          for (int w = 0; w < 4; w++) B[w] = P[b][w];  // GHASH over the ciphertext input
+          for (int w = 0; w < 4; w++) B[w] = P[w];  // GHASH over the ciphertext input
           if (tls) {
             const int j = last_nonzero(C, (int)valid);
             if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((C[j >> 2] >> (8 * (j & 3))) & 0xffu);
@@ -307,11 +396,20 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
         B[0] = bswap32((uint32_t)(abits >> 32)); B[1] = bswap32((uint32_t)abits);
         B[2] = bswap32((uint32_t)(cbits >> 32)); B[3] = bswap32((uint32_t)cbits);
       }
-      ghash_mul_tab(y, wb);
-#pragma unroll
-      for (int w = 0; w < 4; w++) y[w] ^= B[w];
     }
+    // Y <- Y * H^64 ^ B on the lanes that hold a GHASH block; the others keep Y (s_last below).
+    uint32_t yn[4] = {y[0], y[1], y[2], y[3]};
+    ghash_mul<ATLS_GHASH_W>(yn, wb);
+    if (s >= 1 && s <= m) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) y[w] = yn[w] ^ B[w];
+    }
+#ifdef ATLS_TT_STAMPS
+    t_gen += __builtin_amdgcn_s_memtime() - t_step;
+    n_gen++;
+#endif
   }
+  TT_STAMP(t_loop);
 
   // ---- lane combine: Z = sum_l Y_l * H^(S - s_last(l)) ----
   uint32_t z[4] = {0, 0, 0, 0};
@@ -354,6 +452,18 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       write_open_result(A, rec_idx, tls, len, ok, lastnz);
     }
   }
+#ifdef ATLS_TT_STAMPS
+  TT_STAMP(t_end);
+  if (lane == 0) {
+    atomicAdd(&g_tt_stamps[0], (unsigned long long)(t_setup - t_start));
+    atomicAdd(&g_tt_stamps[1], (unsigned long long)t_fast);
+    atomicAdd(&g_tt_stamps[2], (unsigned long long)t_gen);
+    atomicAdd(&g_tt_stamps[3], (unsigned long long)(t_end - t_loop));
+    atomicAdd(&g_tt_stamps[4], 1ull);
+    atomicAdd(&g_tt_stamps[5], (unsigned long long)n_fast);
+    atomicAdd(&g_tt_stamps[6], (unsigned long long)n_gen);
+  }
+#endif
 }
 
 // WAVES waves per workgroup (one record per wave at a time), one workgroup per CU: the LDS
@@ -364,8 +474,8 @@ template <bool OPEN, int kWaves, int NR>
 __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A, uint32_t report) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
-    const uint32_t v = A.t0[i >> (kNTab == 2 ? 6 : 5)];
-    smem[i] = (kNTab == 2 && (i & 32)) ? rotl32(v, 8) : v;  // row x: T0[x] x32 (| T1[x] x32)
+    const uint32_t v = A.t0[i >> 6];
+    smem[i] = (i & 32) ? rotl32(v, 8) : v;  // row x: T0[x] x32 | T1[x] x32
   }
   __syncthreads();
   const int wave = (int)uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -418,7 +528,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;
-    return (w == 4 || w == 8 || w == 12 || (atls::kNTab == 1 && w == 16)) ? w : 12;
+    return (w == 4 || w == 8 || w == 12) ? w : 12;
   }();
   uint32_t want = (n + waves - 1) / waves;
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
@@ -437,8 +547,21 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
     if (nr_mask & 4) { ATLS_LAUNCH_NR(W, 14) }         \
   }
   ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(12)
-  if constexpr (atls::kNTab == 1) { ATLS_LAUNCH(16) }
 #undef ATLS_LAUNCH
 #undef ATLS_LAUNCH_NR
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}
+
+// Debug: copy out (and reset) the phase timers of a -DATLS_TT_STAMPS build; -1 otherwise.
+extern "C" int atls_debug_tt_stamps(unsigned long long* out) {
+#ifdef ATLS_TT_STAMPS
+  unsigned long long h[8], z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(atls::g_tt_stamps), sizeof(h)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(atls::g_tt_stamps), z, sizeof(z)) != hipSuccess) return -1;
+  for (int i = 0; i < 8; i++) out[i] = h[i];
+  return 0;
+#else
+  (void)out;
+  return -1;
+#endif
 }

@@ -106,6 +106,7 @@ __global__ void key_setup_kernel(const atls_key* __restrict__ keys, uint32_t n, 
     o->rk[w] = w < 4 * (nr + 1) ? ((uint32_t)ek[4 * w] | ((uint32_t)ek[4 * w + 1] << 8) |
                                    ((uint32_t)ek[4 * w + 2] << 16) | ((uint32_t)ek[4 * w + 3] << 24))
                                 : 0u;
+  for (int w = 0; w < 60; w++) o->rkr[w] = (o->rk[w] << 16) | (o->rk[w] >> 16);
   o->nr = (uint32_t)nr;
   // H = E_K(0) (gcm.rs:56) and its powers.
   uint8_t zero[16] = {0}, hb[16];
