@@ -28,6 +28,9 @@ namespace atls {
 #ifndef ATLS_GHASH_W
 #define ATLS_GHASH_W 0  // > 0: GHASH lookups issued per LDS round trip (ghash_mul_tab_wide); 0: compiler schedule
 #endif
+#ifndef ATLS_DBG_SKIP
+#define ATLS_DBG_SKIP 0  // timing experiments only (wrong results): 1 lane combine, 2 general steps, 4 GHASH table
+#endif
 #ifndef ATLS_CTR_CACHE
 #define ATLS_CTR_CACHE 1
 #endif
@@ -245,7 +248,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     uint32_t seed[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) seed[w] = k->p4_be[lane >> 1][w];
-    ghash_table_entries<8>(wb, seed, lane >> 1, (lane & 1) * 8);
+    if (!(ATLS_DBG_SKIP & 4)) ghash_table_entries<8>(wb, seed, lane >> 1, (lane & 1) * 8);
   }
   wave_lds_sync();
 
@@ -310,6 +313,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 #endif
       continue;
     }
+    if (ATLS_DBG_SKIP & 2) continue;
     // counter block J0 + c (gcm.rs:89-96): c = s - na for data block s - 1 - na, 0 for slots 0..na
     const uint32_t c = (s > na) ? (s - na) : 0u;
     uint32_t cb[4] = {j0[0], j0[1], j0[2], j0[3]};
@@ -418,13 +422,18 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     int64_t s_last = -1;
     if (l == 0) { if (m >= 64) s_last = (int64_t)(m / 64) * 64; }
     else if (l <= m) s_last = (int64_t)l + (int64_t)((m - l) / 64) * 64;
-    if (s_last >= 1) {
+    if (s_last >= 1 && !(ATLS_DBG_SKIP & 1)) {
       const uint32_t e = S - (uint32_t)s_last;  // 1..64
       const uint32_t yb[4] = {bswap32(y[0]), bswap32(y[1]), bswap32(y[2]), bswap32(y[3])};
       uint32_t hp[4];
 #pragma unroll
-      for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e - 1][w];
-      gf_mul_be(yb, hp, z);
+      for (int w = 0; w < 4; w++) hp[w] = (ATLS_DBG_SKIP & 8) ? yb[w] * (e + w) : k->hpow_be[e - 1][w];
+      if (ATLS_DBG_SKIP & 16) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) z[w] = yb[w] ^ hp[w];
+      } else {
+        gf_mul_comb(yb, hp, z);
+      }
     }
   }
 #pragma unroll

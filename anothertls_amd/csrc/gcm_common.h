@@ -120,6 +120,41 @@ __device__ __forceinline__ void ghash_mul_tab_wide(uint32_t (&y)[4], uint32_t wb
   y[0] = a0; y[1] = a1; y[2] = a2; y[3] = a3;
 }
 
+// z = x * p in GF(2^128), be words: the same product as gf_mul_be (gcm.rs:21-40 gmult), as a
+// transposed comb. With Q_w = p * X^(32w) and c(i) the coefficient of X^i in x (bit 31 - i%32 of
+// word i/32): x*p = sum_{j<32} X^j * T_j, T_j = sum_w c(32w + j) Q_w. Horner over j = 31..0 costs
+// one multiply-by-X and 16 masked XORs per j: 32 iterations instead of gf_mul_be's 128.
+__device__ __forceinline__ void gf_mul_comb(const uint32_t (&x)[4], const uint32_t (&p)[4], uint32_t (&z)[4]) {
+  uint32_t q[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) q[0][c] = p[c];
+#pragma unroll
+  for (int t = 1; t < 4; t++) {  // q[t] = q[t-1] * X^32: word shift; word 3 folds back via X^128 = 1+X+X^2+X^7
+    const uint32_t w = q[t - 1][3];
+    q[t][0] = w ^ (w >> 1) ^ (w >> 2) ^ (w >> 7);
+    q[t][1] = q[t - 1][0] ^ (w << 31) ^ (w << 30) ^ (w << 25);
+    q[t][2] = q[t - 1][1];
+    q[t][3] = q[t - 1][2];
+  }
+  uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+#pragma unroll
+  for (int j = 31; j >= 0; j--) {
+    if (j < 31) {  // z <- z * X
+      const uint32_t r = (uint32_t)((int32_t)(z3 << 31) >> 31) & 0xE1000000u;
+      z3 = __builtin_amdgcn_alignbit(z2, z3, 1);
+      z2 = __builtin_amdgcn_alignbit(z1, z2, 1);
+      z1 = __builtin_amdgcn_alignbit(z0, z1, 1);
+      z0 = (z0 >> 1) ^ r;
+    }
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const uint32_t m = (uint32_t)((int32_t)(x[w] << j) >> 31);  // c(32w + j): bit 31 - j of x[w]
+      z0 ^= m & q[w][0]; z1 ^= m & q[w][1]; z2 ^= m & q[w][2]; z3 ^= m & q[w][3];
+    }
+  }
+  z[0] = z0; z[1] = z1; z[2] = z2; z[3] = z3;
+}
+
 // ---- byte helpers for partial / unaligned blocks -------------------------------------------
 __device__ __forceinline__ void put_byte(uint32_t w[4], int q, uint32_t v) { w[q >> 2] |= v << (8 * (q & 3)); }
 __device__ __forceinline__ uint32_t get_byte(const uint32_t w[4], int q) { return (w[q >> 2] >> (8 * (q & 3))) & 0xffu; }

@@ -21,6 +21,12 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, unsigned long long* clk,
         if (OP == 1) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[i]) : "v"(b), "v"(c));
         if (OP == 2) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(a[i]) : "v"(b));
         if (OP == 3) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
+        if (OP == 5) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "v"(b));
+        if (OP == 6) asm volatile("v_mul_hi_u32_u24 %0, %0, %1" : "+v"(a[i]) : "v"(b));
+        if (OP == 7) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "v"(b));
+        if (OP == 8) { uint64_t t; asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(t) : "v"(a[i]), "v"(b)); a[i] = (uint32_t)t ^ (uint32_t)(t >> 32); }
+        if (OP == 9) asm volatile("v_bfe_i32 %0, %0, %1, 1" : "+v"(a[i]) : "v"(b));
+        if (OP == 10) asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(*(uint64_t*)&a[i & ~1]));
         if (OP == 4) { if (i & 1) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[i]) : "v"(b));
                        else asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[i]) : "v"(b), "v"(c)); }
       }
@@ -55,12 +61,17 @@ int main() {
   uint32_t* dout; unsigned long long* dclk;
   (void)hipMalloc(&dout, 256 * 16 * 256 * 4);
   (void)hipMalloc(&dclk, 64);
-  for (int w : {1, 2, 4}) {
+  for (int w : {2}) {
     run<0>("xor", dout, dclk, w);
     run<1>("bitop3", dout, dclk, w);
     run<2>("alignbit", dout, dclk, w);
     run<3>("perm", dout, dclk, w);
-    run<4>("mix", dout, dclk, w);
+    run<5>("mul_u24", dout, dclk, w);
+    run<6>("mulhi_u24", dout, dclk, w);
+    run<7>("mul_lo_u32", dout, dclk, w);
+    run<8>("mad_u64_u32", dout, dclk, w);
+    run<9>("bfe_i32", dout, dclk, w);
+    run<10>("lshr_b64", dout, dclk, w);
   }
   return 0;
 }
