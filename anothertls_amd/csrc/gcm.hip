@@ -281,6 +281,13 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     aes_rounds_tt<NR, 3>(st4, rk, rkr, lb);
   };
 
+  // Lane combine exponent (see below): s_last = the lane's last slot holding a GHASH block (slots
+  // 1..m), -1 if none.
+  int64_t s_last = -1;
+  if (lane == 0) { if (m >= 64) s_last = (int64_t)(m / 64) * 64; }
+  else if ((uint32_t)lane <= m) s_last = (int64_t)lane + (int64_t)((m - (uint32_t)lane) / 64) * 64;
+  const uint32_t e_comb = s_last >= 1 ? S - (uint32_t)s_last : 1u;  // 1..64
+
   TT_STAMP(t_setup);
   for (uint32_t base = 0; base < S; base += 64) {
     TT_STAMP(t_step);
@@ -417,30 +424,15 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 
   // ---- lane combine: Z = sum_l Y_l * H^(S - s_last(l)) ----
   uint32_t z[4] = {0, 0, 0, 0};
-  {
-    const uint32_t l = (uint32_t)lane;
-    int64_t s_last = -1;
-    if (l == 0) { if (m >= 64) s_last = (int64_t)(m / 64) * 64; }
-    else if (l <= m) s_last = (int64_t)l + (int64_t)((m - l) / 64) * 64;
-    if (s_last >= 1 && !(ATLS_DBG_SKIP & 1)) {
-      const uint32_t e = S - (uint32_t)s_last;  // 1..64
-      const uint32_t yb[4] = {bswap32(y[0]), bswap32(y[1]), bswap32(y[2]), bswap32(y[3])};
-      uint32_t hp[4];
+  if (s_last >= 1) {
+    uint32_t hp[4];
 #pragma unroll
-      for (int w = 0; w < 4; w++) hp[w] = (ATLS_DBG_SKIP & 8) ? yb[w] * (e + w) : k->hpow_be[e - 1][w];
-      if (ATLS_DBG_SKIP & 16) {
-#pragma unroll
-        for (int w = 0; w < 4; w++) z[w] = yb[w] ^ hp[w];
-      } else {
-        gf_mul_comb(yb, hp, z);
-      }
-    }
+    for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e_comb - 1][w];
+    const uint32_t yb[4] = {bswap32(y[0]), bswap32(y[1]), bswap32(y[2]), bswap32(y[3])};
+    gf_mul_comb(yb, hp, z);
   }
 #pragma unroll
-  for (int off = 32; off >= 1; off >>= 1) {
-#pragma unroll
-    for (int w = 0; w < 4; w++) z[w] ^= __shfl_xor(z[w], off, 64);
-  }
+  for (int w = 0; w < 4; w++) z[w] = wave_xor(z[w]);
   const uint32_t t0 = e0 ^ bswap32(z[0]), t1 = e1 ^ bswap32(z[1]), t2 = e2 ^ bswap32(z[2]), t3 = e3 ^ bswap32(z[3]);
 
   if (!OPEN) {

@@ -137,9 +137,10 @@ __device__ __forceinline__ void gf_mul_comb(const uint32_t (&x)[4], const uint32
     q[t][3] = q[t - 1][2];
   }
   uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
-#pragma unroll
+  // Rolled: the unrolled form lets the compiler materialise all 128 masks at once.
+#pragma unroll 1
   for (int j = 31; j >= 0; j--) {
-    if (j < 31) {  // z <- z * X
+    {  // z <- z * X (a no-op on the first pass, z = 0)
       const uint32_t r = (uint32_t)((int32_t)(z3 << 31) >> 31) & 0xE1000000u;
       z3 = __builtin_amdgcn_alignbit(z2, z3, 1);
       z2 = __builtin_amdgcn_alignbit(z1, z2, 1);
@@ -153,6 +154,18 @@ __device__ __forceinline__ void gf_mul_comb(const uint32_t (&x)[4], const uint32
     }
   }
   z[0] = z0; z[1] = z1; z[2] = z2; z[3] = z3;
+}
+
+// XOR of x over the wave without the LDS (ds_bpermute) path of __shfl_xor: four DPP steps leave
+// every lane with its 16-lane row's XOR (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror), then four v_readlane combine the rows. Wave-uniform result.
+__device__ __forceinline__ uint32_t wave_xor(uint32_t x) {
+  x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+  x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+  x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);
+  x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);
+  return (uint32_t)(__builtin_amdgcn_readlane((int)x, 0) ^ __builtin_amdgcn_readlane((int)x, 16) ^
+                    __builtin_amdgcn_readlane((int)x, 32) ^ __builtin_amdgcn_readlane((int)x, 48));
 }
 
 // ---- byte helpers for partial / unaligned blocks -------------------------------------------
