@@ -16,7 +16,7 @@
 
 namespace atls {
 
-// Per key slot device state, built by the key-setup kernel (keysetup.hip). 2624 B, 16-B aligned.
+// Per key slot device state, built by the key-setup kernel (keysetup.hip). 2112 B, 16-B aligned.
 struct alignas(16) KeySched {
   uint32_t suite, nr, key_len, valid;  // nr = AES rounds (10/12/14), 0 for ChaCha
   uint32_t rk[60];                     // AES round keys as raw words (cipher.rs:216-249 expanded_key)
@@ -25,11 +25,10 @@ struct alignas(16) KeySched {
   uint32_t h_be[4];                    // H = E_K(0^128) (gcm.rs:56)
   uint32_t hpow_be[64][4];             // H^(i+1), i = 0..63: lane-combine multipliers
   uint32_t p4_be[32][4];               // x^(4p) * H^64, p = 0..31: seeds of the 4-bit GHASH tables
-  uint32_t p4h32_be[32][4];            // x^(4p) * H^32: the same for the bitsliced kernel's stride
   uint32_t rkr[60];                    // rotl16(rk[i]): the T-table rounds' key words (gcm.hip)
   uint32_t pad[4];
 };
-static_assert(sizeof(KeySched) == 2624, "KeySched must be 2624 B");
+static_assert(sizeof(KeySched) == 2112, "KeySched must be 2112 B");
 
 constexpr int kSuiteAes128 = 0x1301, kSuiteAes256 = 0x1302, kSuiteChacha = 0x1303;
 

@@ -15,7 +15,7 @@
 // with r^(4G) = r^64; each lane's partial is finally multiplied by r^e (e in 1..65, square-
 // and-multiply over r^(2^b)) and the group sums the partials mod p.
 // Bytes per record (roofline): read L, write L + 16.
-#include "atls_dev.h"
+#include "plan.h"
 
 namespace atls {
 
@@ -127,8 +127,10 @@ struct ChArgs {
   uint8_t* tags_out;
   const uint8_t* tags_in;
   atls_open_result* res;
-  uint32_t* err;
-  uint32_t n_slots;
+  const uint32_t* idx;  // batch plan (plan.hip); nullptr: direct
+  PlanHdr* plan;
+  uint32_t* err;        // direct mode: sticky error word
+  uint32_t n_slots;     // direct mode: key-table size
 };
 
 template <bool OPEN>
@@ -362,38 +364,36 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   }
 }
 
+// The waves take the ChaCha20-Poly1305 work list (plan.hip, longest first) round-robin, 4
+// consecutive positions (records of similar length) per wave and step, one per 16-lane group.
 template <bool OPEN>
 __global__ __launch_bounds__(256) void chacha_kernel(ChArgs A) {
   const int lane = threadIdx.x & 63;
   const int gl = lane & (G - 1);
-  const uint32_t group = (blockIdx.x * blockDim.x + threadIdx.x) / G;
-  const uint32_t stride = gridDim.x * blockDim.x / G;
-  for (uint32_t r = group; r < A.n; r += stride) {
-    const atls_rec d = A.recs[r];
-    if (d.key_slot >= A.n_slots || d.mode > ATLS_MODE_RAW) {
-      if (gl == 0) {
-        atomicOr(A.err, 1u);
-        if (OPEN) {
-          atls_open_result rr = {0, ATLS_ILLEGAL_PARAMETER, 0, {0, 0}};
-          A.res[r] = rr;
+  const uint32_t grp = (uint32_t)(lane / G);
+  const WorkList W{A.idx, A.plan, kListChacha, A.n};
+  const uint32_t cnt = W.size();
+  constexpr uint32_t kPer = 64u / G;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
+  const uint32_t stride = gridDim.x * blockDim.x / 64u * kPer;
+  for (uint32_t q0 = wave * kPer; q0 < cnt; q0 += stride) {
+    const uint32_t q = q0 + grp;
+    if (q < cnt) {
+      const uint32_t r = W.record(q);
+      const atls_rec d = A.recs[r];
+      const uint32_t st = A.idx ? 0u : direct_reject(d, A.ks, A.n_slots);  // direct mode
+      if (st) {
+        if (gl == 0) {
+          atomicOr(A.err, 1u);
+          if (OPEN) {
+            atls_open_result rr = {0, (uint8_t)st, 0, {0, 0}};
+            A.res[r] = rr;
+          }
         }
+      } else {
+        chacha_record<OPEN>(A, d, A.ks + d.key_slot, r, gl);
       }
-      continue;
     }
-    const KeySched* k = A.ks + d.key_slot;
-    if (k->suite != kSuiteChacha) continue;  // AES-GCM records: gcm.hip
-    const bool bad = !k->valid || (d.mode == ATLS_MODE_RAW && d.iv_len != 12);
-    if (bad) {
-      if (gl == 0) {
-        atomicOr(A.err, 1u);
-        if (OPEN) {
-          atls_open_result rr = {0, ATLS_ILLEGAL_PARAMETER, 0, {0, 0}};
-          A.res[r] = rr;
-        }
-      }
-      continue;
-    }
-    chacha_record<OPEN>(A, d, k, r, gl);
   }
 }
 
@@ -401,10 +401,11 @@ __global__ __launch_bounds__(256) void chacha_kernel(ChArgs A) {
 
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
-                                  atls_open_result* res, uint32_t* err, uint32_t n_slots, int grid,
-                                  hipStream_t s) {
+                                  atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
+                                  uint32_t n_slots, int grid, hipStream_t s) {
   if (n == 0) return 0;
-  atls::ChArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, err, n_slots};
+  atls::ChArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, idx,
+                 (atls::PlanHdr*)plan, err, n_slots};
   const uint32_t per_block = 256 / atls::G;
   uint32_t want = (n + per_block - 1) / per_block;
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;

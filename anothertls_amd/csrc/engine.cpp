@@ -1,10 +1,11 @@
 // Host engine + C ABI (include/atls.h). C++ on the HIP runtime; no torch types.
 //
-// The engine owns one HIP device and one stream, the device key-slot table (KeySched, built
+// The engine owns one HIP device and two streams, the device key-slot table (KeySched, built
 // by the key-setup kernel), the AES T-table, and staging buffers for callers that hand over
-// host memory. Batches are dispatched to the AES-GCM and ChaCha20-Poly1305 kernels; each
-// kernel walks the whole descriptor array and takes the records of its suite, so descriptors
-// may stay device-resident (ATLS_FLAG_DEVICE_RECS) with no host-side partitioning.
+// host memory. A batch is first planned on the device (plan.hip: validation, one work list per
+// kernel, longest records first), then the AES-GCM kernel (engine stream) and the
+// ChaCha20-Poly1305 kernel (second stream, joined back) run concurrently over their lists, so
+// descriptors may stay device-resident (ATLS_FLAG_DEVICE_RECS) with no host-side partitioning.
 //
 // atls_seal / atls_open are the Cipher-trait drop-ins (crypto/ciphersuite.rs:12-31): one RAW
 // record through a process-default engine, with the same argument meaning and error codes.
@@ -19,21 +20,21 @@
 
 #include "../../include/atls.h"
 #include "atls_dev.h"
+#include "plan.h"
 
 extern "C" int atls_launch_build_t0(uint32_t* t0, hipStream_t s);
 extern "C" int atls_launch_key_setup(const atls_key* keys, uint32_t n, void* ks, hipStream_t s);
+extern "C" int atls_launch_plan(int open, const void* ks, const atls_rec* recs, uint32_t n, uint32_t n_slots,
+                                atls_open_result* res, uint32_t* err, void* P, uint8_t* keys, uint32_t* idx,
+                                hipStream_t s);
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
-                               atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
-                               int bs_on, int nr_mask, int grid, hipStream_t s);
-extern "C" int atls_launch_gcm_bs(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
-                                  const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
-                                  atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
-                                  int nr_mask, int grid, hipStream_t s);
+                               atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
+                               uint32_t* err, uint32_t n_slots, int nr_mask, int grid, hipStream_t s);
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
-                                  atls_open_result* res, uint32_t* err, uint32_t n_slots, int grid,
-                                  hipStream_t s);
+                                  atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
+                                  uint32_t n_slots, int grid, hipStream_t s);
 extern "C" int atls_launch_derive(uint16_t suite, const uint8_t* secrets, uint32_t secret_len, uint32_t n,
                                   atls_key* out, hipStream_t s);
 
@@ -64,12 +65,15 @@ struct DevBuf {
 struct atls_engine {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;             // ChaCha20-Poly1305 kernel, concurrent with AES-GCM
+  hipEvent_t ev_plan = nullptr, ev_side = nullptr;
   int cus = 256;
   uint32_t n_slots = 0;
   bool has_aes = false, has_chacha = false;  // suites present in the key table: skip idle kernels
   int aes_nr_mask = 0;                       // bit 0/1/2: AES slots with 10/12/14 rounds
-  bool bitsliced = false;                    // ATLS_GCM_BS=1: full-size AES-GCM records go to gcm_bs.hip
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
+  DevBuf plan, plan_keys, plan_idx;          // batch plan (plan.hip)
+  bool force_plan = false;                   // ATLS_FORCE_PLAN=1: plan every batch (tests)
   std::mutex mu;
 };
 
@@ -150,20 +154,41 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   }
   if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
   int rc = 0;
-  const bool bs = e->has_aes && e->bitsliced && e->aes_nr_mask;
-  if (bs)  // the bitsliced kernels take the full-size records, the T-table kernel the rest
-    rc = atls_launch_gcm_bs(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
-                            (const uint32_t*)e->t0.p, (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask, e->cus * 2, s);
-  if (rc) return rc;
+  // A key table holding one record kernel's suite and round count gives a direct batch: that
+  // kernel walks the descriptors itself. Otherwise the batch is planned (plan.hip): ~30 us of
+  // small launches that sort records into per-kernel lists, longest first.
+  const int kinds = (e->has_chacha ? 1 : 0) + __builtin_popcount((unsigned)e->aes_nr_mask);
+  const bool planned = kinds > 1 || e->force_plan;
+  const uint32_t* idx = nullptr;
+  if (planned) {
+    if (!e->plan.reserve(sizeof(atls::PlanHdr)) || !e->plan_keys.reserve(n) || !e->plan_idx.reserve(4 * (size_t)n))
+      return ATLS_INTERNAL_ERROR;
+    rc = atls_launch_plan(open, e->ks.p, d_recs, n, e->n_slots, d_res, (uint32_t*)e->err.p, e->plan.p,
+                          (uint8_t*)e->plan_keys.p, (uint32_t*)e->plan_idx.p, s);
+    if (rc) return rc;
+    idx = (const uint32_t*)e->plan_idx.p;
+  }
+  // Both suites present: ChaCha20-Poly1305 (VALU-bound) on the second stream beside AES-GCM
+  // (LDS-bound), joined back into the engine stream.
+  const bool side = e->has_aes && e->has_chacha;
+  if (e->has_chacha) {
+    hipStream_t cs = s;
+    if (side) {
+      if (hipEventRecord(e->ev_plan, s) != hipSuccess || hipStreamWaitEvent(e->stream2, e->ev_plan, 0) != hipSuccess)
+        return ATLS_INTERNAL_ERROR;
+      cs = e->stream2;
+    }
+    rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, idx,
+                            e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * 8, cs);
+    if (rc) return rc;
+    if (side && hipEventRecord(e->ev_side, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  }
   if (e->has_aes)
     rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
-                         (const uint32_t*)e->t0.p, (uint32_t*)e->err.p, e->n_slots, bs ? 1 : 0, e->aes_nr_mask,
-                         e->cus * 2, s);
+                         (const uint32_t*)e->t0.p, idx, e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask,
+                         e->cus, s);
   if (rc) return rc;
-  if (e->has_chacha)
-    rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
-                            (uint32_t*)e->err.p, e->n_slots, e->cus * 8, s);
-  if (rc) return rc;
+  if (side && hipStreamWaitEvent(s, e->ev_side, 0) != hipSuccess) return ATLS_INTERNAL_ERROR;
   if (!dev_ptrs) {
     if (out_end && hipMemcpyAsync(out, e->out.p, out_end, hipMemcpyDeviceToHost, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
@@ -271,12 +296,19 @@ atls_engine* atls_engine_create(int device) {
   e->device = device;
   hipDeviceProp_t prop;
   if (hipSetDevice(device) != hipSuccess || hipGetDeviceProperties(&prop, device) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_plan, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming) != hipSuccess) {
+    if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);
+    if (e->ev_side) (void)hipEventDestroy(e->ev_side);
+    if (e->stream2) (void)hipStreamDestroy(e->stream2);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
     return nullptr;
   }
   e->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  if (const char* v = std::getenv("ATLS_GCM_BS")) e->bitsliced = std::atoi(v) != 0;  // A/B switch
+  if (const char* v = std::getenv("ATLS_FORCE_PLAN")) e->force_plan = std::atoi(v) != 0;
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
       hipStreamSynchronize(e->stream) != hipSuccess) {
     atls_engine_destroy(e);
@@ -289,9 +321,13 @@ void atls_engine_destroy(atls_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   for (DevBuf* b : {&e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
-                    &e->secrets, &e->dkeys})
+                    &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx})
     b->release();
+  if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);
+  if (e->ev_side) (void)hipEventDestroy(e->ev_side);
+  if (e->stream2) (void)hipStreamDestroy(e->stream2);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -376,3 +412,14 @@ int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, siz
 }
 
 }  // extern "C"
+
+// Debug: copy the last batch plan (PlanHdr words, then the first n_idx record indices) to host.
+extern "C" int atls_debug_plan(atls_engine* e, uint32_t* out, uint32_t n_idx) {
+  if (!e || !e->plan.p) return -1;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e) || hipStreamSynchronize(e->stream) != hipSuccess) return -1;
+  if (hipMemcpy(out, e->plan.p, sizeof(atls::PlanHdr), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (n_idx && hipMemcpy(out + sizeof(atls::PlanHdr) / 4, e->plan_idx.p, 4 * (size_t)n_idx, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return 0;
+}

@@ -468,11 +468,11 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 }
 
 // WAVES waves per workgroup (one record per wave at a time), one workgroup per CU: the LDS
-// footprint (64 KiB tables + 8 KiB per wave) is what limits residency.
-// One launch per AES round count present in the key table (a kernel holds only that count's
-// round keys, in SGPRs); the launch with `report` set also reports the records no launch takes.
+// footprint (64 KiB tables + 8 KiB per wave) is what limits residency. One launch per AES round
+// count (a kernel holds only that count's round keys); the waves take the records of that round
+// count's work list (plan.hip, longest first) round-robin.
 template <bool OPEN, int kWaves, int NR>
-__global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A, uint32_t report) {
+__global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
     const uint32_t v = A.t0[i >> 6];
@@ -482,50 +482,45 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A, uint32_t re
   const int wave = (int)uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t lb = 4u * (uint32_t)(lane & 31);
   const uint32_t wb = (uint32_t)kTabBytes + (uint32_t)wave * kGhashBytes;
+  const WorkList W{A.idx, A.plan, NR == 10 ? kListGcm10 : NR == 12 ? kListGcm12 : kListGcm14, A.n};
+  const uint32_t cnt = uni(W.size());
   const uint32_t stride = gridDim.x * kWaves;
-  for (uint32_t r = blockIdx.x * kWaves + wave; r < A.n; r += stride) {
-    if (uni(bs_taken<OPEN>(A, r))) continue;  // gcm_bs.hip seals / opens this one
+  for (uint32_t q = blockIdx.x * kWaves + wave; q < cnt; q += stride) {
+    const uint32_t r = uni(W.record(q));
     atls_rec d = A.recs[r];
     d.key_slot = uni(d.key_slot);
     d.len = uni(d.len);
     d.mode = (uint8_t)uni(d.mode);
-    uint32_t status = 0;  // != 0: this record fails with that status (reported by one launch)
-    const KeySched* k = A.ks + (d.key_slot < A.n_slots ? d.key_slot : 0u);
-    if (d.key_slot >= A.n_slots || d.mode > ATLS_MODE_RAW) {
-      status = ATLS_ILLEGAL_PARAMETER;
-    } else {
-      const uint32_t suite = uni(k->suite);
-      if (suite == kSuiteChacha) continue;  // ChaCha20-Poly1305 records: chacha.hip
-      if (suite != kSuiteAes128 && suite != kSuiteAes256) status = ATLS_INSUFFICIENT_SECURITY;  // get_cipher (:84)
-      else if (!uni(k->valid)) status = ATLS_ILLEGAL_PARAMETER;
-    }
-    if (status) {
-      if (report && lane == 0) {
-        atomicOr(A.err, 1u);
-        if (OPEN) {
-          atls_open_result rr = {0, (uint8_t)status, 0, {0, 0}};
-          A.res[r] = rr;
+    if (!A.idx) {  // direct mode: reject as the plan would
+      const uint32_t st = uni(direct_reject(d, A.ks, A.n_slots));
+      if (st) {
+        if (lane == 0) {
+          atomicOr(A.err, 1u);
+          if (OPEN) {
+            atls_open_result rr = {0, (uint8_t)st, 0, {0, 0}};
+            A.res[r] = rr;
+          }
         }
+        continue;
       }
-      continue;
     }
-    if (uni(k->nr) != (uint32_t)NR) continue;  // another launch's round count
-    gcm_record<NR, OPEN>(A, d, k, r, lb, wb, lane);
+    gcm_record<NR, OPEN>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
     wave_lds_sync();  // table reads of this record done before the next record rebuilds it
   }
 }
 
 }  // namespace atls
 
-// nr_mask: bit 0/1/2 = key slots with 10/12/14 rounds exist (one launch each; with none, one
-// launch still reports the invalid records).
+// nr_mask: bit 0/1/2 = key slots with 10/12/14 rounds exist (one launch each). plan/idx: the
+// batch plan of atls_launch_plan, or idx = nullptr for a direct batch (one round count only; the
+// kernel validates and reports through err). grid: workgroups per launch (one per CU).
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
-                               atls_open_result* res, const uint32_t* t0, uint32_t* err, uint32_t n_slots,
-                               int bs_on, int nr_mask, int grid, hipStream_t s) {
+                               atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
+                               uint32_t* err, uint32_t n_slots, int nr_mask, int grid, hipStream_t s) {
   if (n == 0) return 0;
-  atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, err, n_slots,
-                  (uint32_t)(bs_on != 0)};
+  atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, idx,
+                  (atls::PlanHdr*)plan, err, n_slots};
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;
@@ -535,12 +530,9 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
   const dim3 block(64 * waves);
   const size_t lds = atls::lds_bytes(waves);
-  if ((nr_mask & 7) == 0) nr_mask = 1;
-  uint32_t report = 1;
-#define ATLS_LAUNCH_NR(W, NR)                                                                           \
-  if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR>), dim3(g), block, lds, s, A, report);     \
-  else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR>), dim3(g), block, lds, s, A, report);         \
-  report = 0;
+#define ATLS_LAUNCH_NR(W, NR)                                                                  \
+  if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR>), dim3(g), block, lds, s, A);    \
+  else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR>), dim3(g), block, lds, s, A);
 #define ATLS_LAUNCH(W)                                 \
   if (waves == W) {                                    \
     if (nr_mask & 1) { ATLS_LAUNCH_NR(W, 10) }         \

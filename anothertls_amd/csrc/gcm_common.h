@@ -3,7 +3,7 @@
 // byte helpers for partial blocks, the kernel argument block, and the rule that splits a
 // batch between the two kernels.
 #pragma once
-#include "atls_dev.h"
+#include "plan.h"
 
 namespace atls {
 
@@ -196,9 +196,10 @@ struct GcmArgs {
   const uint8_t* tags_in;  // open
   atls_open_result* res;   // open
   const uint32_t* t0;      // 256-entry T-table in global memory
-  uint32_t* err;           // sticky error word
-  uint32_t n_slots;        // key-table size: descriptors are bounds-checked on the device
-  uint32_t bs_on;          // 1: records bs_taken() accepts go to the bitsliced kernel
+  const uint32_t* idx;     // batch plan (plan.hip): record indices per work list; nullptr: direct
+  PlanHdr* plan;
+  uint32_t* err;           // direct mode: sticky error word
+  uint32_t n_slots;        // direct mode: key-table size
 };
 
 // Open result for one record (record.rs:203-240 decrypt + padding scan). lastnz = (position <<
@@ -223,39 +224,6 @@ __device__ __forceinline__ void write_open_result(const GcmArgs& A, uint32_t rec
     r.content_type = valid_type ? (uint8_t)ty : 0;
   }
   A.res[rec_idx] = r;
-}
-
-// ---- batch split between the kernels --------------------------------------------------------
-// The bitsliced kernel runs whole 1024-block passes (32 lanes x 32 blocks) per record. A
-// record qualifies when those passes hold only full, aligned data blocks (plus E_K(J0)), the
-// few blocks after them (<= 2 per lane: partial block, length block) fit the scalar tail, the
-// nonce is 96-bit and the AAD is at most 32 blocks. Returns the AES round count, 0 if not.
-constexpr uint32_t kBsPass = 1024;
-template <bool OPEN>
-__device__ __forceinline__ uint32_t bs_class(const GcmArgs& A, const atls_rec& d) {
-  if (d.key_slot >= A.n_slots || d.mode > ATLS_MODE_RAW) return 0;
-  const KeySched* k = A.ks + d.key_slot;
-  if (!k->valid || (k->suite != (uint32_t)kSuiteAes128 && k->suite != (uint32_t)kSuiteAes256)) return 0;
-  const bool tls = d.mode == ATLS_MODE_TLS;
-  if (!tls && (d.iv_len != 12 || d.aad_len > 512)) return 0;
-  const uint32_t n_aead = (tls && !OPEN) ? d.len + 1 : d.len;
-  const uint32_t full = d.len / 16u;  // min(len, n_aead) / 16
-  const uint32_t passes = (full + 1u) / kBsPass;
-  if (passes == 0) return 0;
-  const uint32_t nb = (n_aead + 15u) / 16u;
-  if (nb + 2u - kBsPass * passes > 64u) return 0;
-  if (((uintptr_t)(A.in + d.in_off) | (uintptr_t)(A.out + d.out_off)) & 15u) return 0;
-  return k->nr;
-}
-// Records are paired (2q, 2q+1) onto one wave; a pair runs one round count, so the odd record
-// of a pair whose even record takes a different one is left to the T-table kernel.
-template <bool OPEN>
-__device__ __forceinline__ uint32_t bs_taken(const GcmArgs& A, uint32_t r) {
-  if (!A.bs_on) return 0;
-  const uint32_t c = bs_class<OPEN>(A, A.recs[r]);
-  if (c == 0 || (r & 1u) == 0) return c;
-  const uint32_t c0 = bs_class<OPEN>(A, A.recs[r - 1]);
-  return (c0 != 0 && c0 != c) ? 0u : c;
 }
 
 }  // namespace atls

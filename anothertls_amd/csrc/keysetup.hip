@@ -128,12 +128,6 @@ __global__ void key_setup_kernel(const atls_key* __restrict__ keys, uint32_t n, 
     for (int w = 0; w < 4; w++) o->p4_be[j][w] = v[w];
     gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v);
   }
-  // p4h32[j] = x^(4j) * H^32
-  for (int w = 0; w < 4; w++) v[w] = o->hpow_be[31][w];
-  for (int j = 0; j < 32; j++) {
-    for (int w = 0; w < 4; w++) o->p4h32_be[j][w] = v[w];
-    gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v);
-  }
   o->valid = 1;
 }
 

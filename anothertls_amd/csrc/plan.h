@@ -1,0 +1,46 @@
+// Work lists of a batch (plan.hip) as the record kernels read them.
+#pragma once
+#include "atls_dev.h"
+
+namespace atls {
+
+constexpr uint32_t kListGcm10 = 0, kListGcm12 = 1, kListGcm14 = 2, kListChacha = 3;
+constexpr int kPlanLists = 4;
+constexpr int kPlanClasses = 16;  // length classes min(len >> 10, 15), longest first
+constexpr uint32_t kPlanReject = 0xffu;
+
+struct PlanHdr {
+  uint32_t off[kPlanLists + 1];                  // list l = idx[off[l] .. off[l+1])
+  uint32_t next[kPlanLists];                     // unused (kept zero)
+  uint32_t count[kPlanLists * kPlanClasses];     // plan_count
+  uint32_t cursor[kPlanLists * kPlanClasses];    // plan_scatter
+};
+
+// The record kernels' view: list `l` of the plan. Workers (waves or lane groups) take positions
+// round-robin: worker w of W takes w, w + W, w + 2W, ... of a list ordered longest first, so every
+// worker gets a similar mix of lengths. (A shared atomic fetch counter was measured 2-6x slower:
+// device-scope atomics on one address serialise at the memory side.)
+// idx == nullptr: no plan ("direct" batches whose key table holds one record kernel's suite and
+// round count only): position q is record q and the kernel validates descriptors itself.
+struct WorkList {
+  const uint32_t* idx;  // record indices, longest first
+  PlanHdr* P;
+  uint32_t list;
+  uint32_t n;           // batch size (direct mode)
+
+  __device__ __forceinline__ uint32_t size() const { return idx ? P->off[list + 1] - P->off[list] : n; }
+  __device__ __forceinline__ uint32_t record(uint32_t pos) const { return idx ? idx[P->off[list] + pos] : pos; }
+};
+
+// Direct mode: the status a record gets in place of sealing / opening (0 = process it), as
+// plan_key would give it (plan.hip).
+__device__ __forceinline__ uint32_t direct_reject(const atls_rec& d, const KeySched* ks, uint32_t n_slots) {
+  if (d.key_slot >= n_slots || d.mode > ATLS_MODE_RAW) return ATLS_ILLEGAL_PARAMETER;
+  const KeySched* k = ks + d.key_slot;
+  const uint32_t suite = k->suite;
+  if (suite == (uint32_t)kSuiteChacha) return (!k->valid || (d.mode == ATLS_MODE_RAW && d.iv_len != 12)) ? ATLS_ILLEGAL_PARAMETER : 0;
+  if (suite == (uint32_t)kSuiteAes128 || suite == (uint32_t)kSuiteAes256) return k->valid ? 0 : ATLS_ILLEGAL_PARAMETER;
+  return ATLS_INSUFFICIENT_SECURITY;
+}
+
+}  // namespace atls

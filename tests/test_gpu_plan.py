@@ -1,0 +1,98 @@
+"""GPU: the batch plan (anothertls_amd/csrc/plan.hip). A key table with several record kernels
+(AES-128, AES-256, ChaCha20-Poly1305) plans every batch: each record lands in its kernel's work
+list, lists ordered by length class longest first; rejected records get their status. Results
+are checked against the oracle in both planned and direct (single-kernel key table) batches."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def atls():
+    import anothertls_amd as a
+
+    if not a.device_available():
+        pytest.skip("no HIP device")
+    return a
+
+
+def _plan(atls, eng, n):
+    lib = atls.library()
+    lib.atls_debug_plan.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]
+    hdr_words = 5 + 4 + 64 + 64
+    buf = (ctypes.c_uint32 * (hdr_words + n))()
+    assert lib.atls_debug_plan(eng._e, buf, n) == 0
+    w = np.frombuffer(buf, np.uint32)
+    return w[:5].copy(), w[hdr_words:].copy()
+
+
+def test_plan_lists_and_order(atls):
+    import oracle as ora
+    from anothertls_amd import workload
+
+    rng = np.random.default_rng(7)
+    n = 600
+    suites = np.array([0x1301, 0x1302, 0x1303], np.uint16)
+    lens = rng.integers(0, 16385, n).astype(np.uint64)
+    b = workload.tls_batch(n, lens, lambda k: suites[np.arange(k) % 3], n_keys=3)
+    recs = b["recs"].copy()
+    eng = atls.Engine(0)
+    eng.set_keys(b["keys"])
+    inbuf = rng.integers(0, 256, b["in_bytes"], dtype=np.uint8)
+    out = np.zeros(b["out_bytes"], np.uint8)
+    tags = np.zeros(16 * n, np.uint8)
+    eng.seal_batch(recs, inbuf, np.zeros(16, np.uint8), out, tags)
+    off, idx = _plan(atls, eng, n)
+    slot = recs["key_slot"]
+    want = {0: np.flatnonzero(slot == 0), 2: np.flatnonzero(slot == 1), 3: np.flatnonzero(slot == 2)}  # AES-256: 14 rounds
+    assert off[4] == n
+    for lst, members in want.items():
+        got = idx[off[lst]:off[lst + 1]]
+        assert sorted(got.tolist()) == sorted(members.tolist()), lst
+        cls = np.minimum(recs["len"][got] >> 10, 15)
+        assert (np.diff(cls.astype(np.int64)) <= 0).all(), "longest class first"
+    assert off[1] == off[2]  # no 12-round keys
+    # every accepted record sealed exactly as the oracle does
+    okeys = (ora.OraKey * 3).from_buffer_copy(b["keys"].tobytes())
+    orecs = (ora.OraRec * n).from_buffer_copy(recs.tobytes())
+    oout, otags = np.zeros_like(out), np.zeros_like(tags)
+    ora.seal_batch(okeys, orecs, inbuf, np.zeros(16, np.uint8), oout, otags, 8)
+    assert np.array_equal(out, oout) and np.array_equal(tags, otags)
+    eng.close()
+
+
+@pytest.mark.parametrize("planned", [False, True])
+def test_rejected_records_device_descriptors(atls, planned):
+    """Device-resident descriptors skip the host-side check: the plan (or, for a direct batch,
+    the kernel) rejects a bad key slot / mode / suite and opens report the status per record."""
+    torch = pytest.importorskip("torch")
+    from anothertls_amd import workload
+
+    n = 64
+    suite_of = (lambda k: np.where(np.arange(k) % 2 == 0, 0x1301, 0x1303).astype(np.uint16)) if planned else 0x1301
+    b = workload.tls_batch(n, 1000, suite_of, n_keys=4)
+    recs = b["recs"].copy()
+    recs["key_slot"][3] = 77  # out of range
+    recs["mode"][9] = 5       # unknown mode
+    dev = torch.device("cuda", 0)
+    eng = atls.Engine(0)
+    eng.set_keys(b["keys"])
+    d_in = torch.randint(0, 256, (b["out_bytes"] + 64,), dtype=torch.uint8, device=dev)
+    d_out = torch.zeros(b["out_bytes"] + 64, dtype=torch.uint8, device=dev)
+    d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=dev)
+    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+    d_res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
+    d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
+    with pytest.raises(atls.TlsError) as ei:
+        eng.open_batch(d_recs.data_ptr(), d_in, d_aux, d_tags, d_out, d_res,
+                       flags=atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS, n=n)
+    assert ei.value.code == atls.TlsError.ILLEGAL_PARAMETER
+    res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
+    assert res["status"][3] == atls.TlsError.ILLEGAL_PARAMETER and res["status"][9] == atls.TlsError.ILLEGAL_PARAMETER
+    # the other records were opened (random tags: DecryptError in TLS mode)
+    others = np.setdiff1d(np.arange(n), [3, 9])
+    assert (res["status"][others] == atls.TlsError.DECRYPT_ERROR).all()
+    eng.close()
