@@ -170,7 +170,9 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   const uint32_t Q = na + nct + 1u;             // Poly1305 blocks
   const bool f4 = (n % 64u) == 0u;              // cipher.rs:100-102: last block not XORed
 
-  P130 r = p_zero(), rp[7];  // rp[b] = r^(2^b)
+  // r powers: r, rsq = r^2, rcu = r^3 in every lane; R = (r^4)^(gl+1) by a prefix-product scan over the 16
+  // lanes of the group (4 levels); r64 = r^64 (lane 15's R).
+  P130 r = p_zero(), rsq = p_zero(), rcu = p_zero(), R = p_zero(), r64 = p_zero();
   uint32_t sk[4] = {0, 0, 0, 0};
   P130 acc = p_zero(), innerL = p_zero();
   int64_t lastnz = -1;
@@ -190,9 +192,18 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       r.l[2] = ((r1 >> 20) | (r2 << 12)) & M26;
       r.l[3] = ((r2 >> 14) | (r3 << 18)) & M26;
       r.l[4] = r3 >> 8;
-      rp[0] = r;
+      rsq = p_mul(r, r);
+      rcu = p_mul(rsq, r);
+      R = p_mul(rsq, rsq);  // r^4
 #pragma unroll
-      for (int b = 1; b < 7; b++) rp[b] = p_mul(rp[b - 1], rp[b - 1]);
+      for (int d = 1; d < G; d <<= 1) {  // Hillis-Steele prefix product
+        P130 t;
+#pragma unroll
+        for (int i = 0; i < 5; i++) t.l[i] = __shfl_up(R.l[i], (unsigned)d, G);
+        const P130 m = p_mul(R, t);
+        if (gl >= d) R = m;
+      }
+      r64 = shfl_p(R, G - 1);
     }
     if (!active) continue;
 
@@ -208,7 +219,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
           for (int q = 0; q < 16; q++)
             if (16 * i + q < aad_len) B[q >> 2] |= (uint32_t)aadp[16 * i + q] << (8 * (q & 3));
         }
-        inner = p_mul(inner, r);
+        if (cnt) inner = p_mul(inner, r);
         p_add_block(inner, B[0], B[1], B[2], B[3]);
         cnt++;
       }
@@ -283,11 +294,11 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       for (int u = 0; u < 4; u++) {
         const uint32_t c = 4u * (j - 1) + u;
         if (c < nct) {
-          inner = p_mul(inner, r);
+          if (u) inner = p_mul(inner, r);  // piece u = 0 starts the slot's Horner
           p_add_block(inner, C[4 * u], C[4 * u + 1], C[4 * u + 2], C[4 * u + 3]);
           cnt++;
         } else if (c == nct) {  // le64(aad_len) || le64(ct_len) (poly1305.rs:63-64)
-          inner = p_mul(inner, r);
+          if (u) inner = p_mul(inner, r);
           p_add_block(inner, tls ? 5u : aad_len, 0u, n, 0u);
           cnt++;
         }
@@ -296,7 +307,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     if (j == jL) {
       innerL = inner;  // ref = Q-1: contributes inner * r^1
     } else {
-      acc = p_mul(acc, rp[6]);  // r^(4G) = r^64
+      if (base) acc = p_mul(acc, r64);  // r^(4G) = r^64; a lane's first slot is in the first step
       p_add(acc, inner);
     }
     (void)cnt;
@@ -310,13 +321,13 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       const uint32_t jf = l + ((jL - 1 - l) / G) * G;
       const uint32_t ref = (jf == 0) ? na - 1u : na + 4u * jf - 1u;
       const uint32_t e = Q - ref;  // 1..65
-      P130 pw = p_zero();
-      pw.l[0] = 1;
-#pragma unroll
-      for (int b = 0; b < 7; b++) {
-        P130 t = p_mul(pw, rp[b]);
-        if ((e >> b) & 1u) pw = t;
-      }
+      // r^e = r^(e mod 4) * (r^4)^(e >> 2); (r^4)^u is lane u-1's R
+      const uint32_t u = e >> 2, c = e & 3u;
+      P130 ru = shfl_p(R, (int)(u ? u - 1u : 0u));
+      if (u == 0) { ru = p_zero(); ru.l[0] = 1; }
+      P130 pw;
+      if (c == 0) pw = ru;
+      else pw = p_mul(ru, c == 1 ? r : c == 2 ? rsq : rcu);
       if (!(jf == 0 && na == 0)) contrib = p_mul(acc, pw);
     }
     if (l == jL % G) p_add(contrib, p_mul(innerL, r));
