@@ -64,6 +64,40 @@ def whole_job_rate(bytes_per_rank, steps, wall, world):
     return world * bytes_per_rank * steps / wall / 2**30
 
 
+def scatter_gather(nbytes, device=None, reps=3):
+    """Time the exchange the bulk path needs when a batch arrives at one rank:
+    rank 0 scatters `nbytes` of records to every rank and gathers `nbytes` of sealed output back
+    (torch.distributed scatter / gather: RCCL over xGMI for "nccl", gloo on CPU). Not on the
+    timed sealing path. Returns (scatter_GBps, gather_GBps) of the bytes leaving / entering rank
+    0 for the other ranks, max time over ranks, or None for a single rank."""
+    if not (tdist.is_available() and tdist.is_initialized()):
+        return None
+    rank, world = tdist.get_rank(), tdist.get_world_size()
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    parts = [torch.full((nbytes,), r, dtype=torch.uint8, device=device) for r in range(world)] if rank == 0 else None
+
+    def sync():
+        if device is not None and device.type == "cuda":
+            torch.cuda.synchronize(device)
+
+    def timed(fn):
+        fn()  # warm-up (communicator, buffers)
+        sync()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        sync()
+        return max_over_ranks((time.perf_counter() - t0) / reps, device)
+
+    ts = timed(lambda: tdist.scatter(buf, scatter_list=parts, src=0))
+    if not bool((buf == rank).all()):
+        raise RuntimeError("scatter delivered the wrong shard")
+    tg = timed(lambda: tdist.gather(buf, gather_list=parts, dst=0))
+    moved = (world - 1) * nbytes / 1e9
+    return moved / ts, moved / tg
+
+
 def close():
     if tdist.is_available() and tdist.is_initialized():
         barrier()

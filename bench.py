@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16,
                    help="CPU-baseline threads (the GPU box's host share is 16 cores)")
     p.add_argument("--pcie", action="store_true", help="also time host-memory (PCIe-inclusive) batches")
+    p.add_argument("--no-scatter", action="store_true", help="N > 1: skip the RCCL scatter/gather timing")
     return p.parse_args()
 
 
@@ -181,6 +182,19 @@ def main():
             for _ in range(3):
                 eng.seal_batch(recs, h_in, np.zeros(16, np.uint8), h_out, h_tags)
             result["pcie_inclusive_GiBps"] = round(3 * payload / (time.perf_counter() - t0) / 2**30, 3)
+    if world > 1 and not args.no_scatter:
+        # host-arrival exchange beside the sealing path: rank 0 scatters / gathers a
+        # 64 MiB shard per rank over RCCL; reported, not part of `value`
+        try:
+            sg = dist.scatter_gather(64 << 20, dev)
+        except Exception as exc:  # the bench line must survive a collective failure
+            sg = None
+            print(f"scatter/gather measurement failed: {exc}", file=sys.stderr, flush=True)
+        if rank == 0 and result is not None:
+            result["scatter_gather"] = None if sg is None else {
+                "scatter_GBps": round(sg[0], 1), "gather_GBps": round(sg[1], 1), "bytes_per_rank": 64 << 20,
+                "backend": "nccl (RCCL over xGMI)"}
+    if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
     dist.close()

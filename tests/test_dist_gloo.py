@@ -50,6 +50,9 @@ def _worker(rank, world, port, q):
     wall = dist.timed_steps(lambda: calls.append(1), steps=5, warmup=2, sync=lambda: None)
     # rank 1 reports a longer time: the max must win on every rank
     mx = dist.max_over_ranks(1.0 + rank)
+    # bench.py's scatter/gather timing (RCCL on the GPU box): shards arrive intact, rates > 0
+    sg = dist.scatter_gather(1 << 16)
+    assert sg is not None and sg[0] > 0 and sg[1] > 0
     gathered = [None] * world
     tdist.all_gather_object(gathered, (batch["recs"].tobytes(), inbuf.tobytes(), out.tobytes(), tags.tobytes()))
     q.put((rank, len(calls), wall, mx, gathered if rank == 0 else None))

@@ -1,0 +1,171 @@
+"""BASELINE.json config C1: server_https-style loopback. A 1 MiB response body goes out as 64
+TLS 1.3 records of 16 KiB (TLS_AES_128_GCM_SHA256) over a TCP socket on 127.0.0.1: the server
+thread seals and writes, the client reads, splits the stream into records and opens them.
+Keys: RFC 8448 §3 server handshake traffic secret -> write key / iv (Key::from_hkdf,
+net/key_schedule.rs:40-50), sequence numbers 0..63.
+
+Two implementations of the same loop, each checked end to end (body and content types):
+  * gpu  — atls_derive_keys + one atls_seal_batch / atls_open_batch per body (anothertls_amd),
+           framing with anothertls_amd.record (net/record.rs:81-114);
+  * cpu  — the reference's per-record path as the oracle restates it (oracle/ref_restatement.c
+           ora_record_seal / ora_record_open, one record per call like tls_write / tls_read).
+Prints one JSON line: MB/s of body through seal -> socket -> open for each.
+python tools/c1_loopback.py [--reps N] [--cpu-only]"""
+import argparse
+import json
+import os
+import socket
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+SECRET = bytes.fromhex("b67b7d690cc16c4e75e54213cb2d37b4e9c912bcded9105d42befd59d391ad38")  # RFC 8448 §3
+N_REC, CONTENT = 64, 16384
+
+
+def _pair():
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(1)
+    cli = socket.create_connection(srv.getsockname())
+    conn, _ = srv.accept()
+    srv.close()
+    for s in (cli, conn):
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
+        s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
+    return conn, cli
+
+
+def _recv_exact(sock, n):
+    buf = bytearray(n)
+    view, got = memoryview(buf), 0
+    while got < n:
+        k = sock.recv_into(view[got:], n - got)
+        if not k:
+            raise ConnectionError("peer closed")
+        got += k
+    return bytes(buf)
+
+
+def _loop(seal_body, open_wire, wire_len, reps):
+    """reps x (server: seal + send | client: recv + open); returns (seconds, last plaintext)."""
+    server, client = _pair()
+    out = {}
+
+    def serve():
+        for _ in range(reps):
+            server.sendall(seal_body())
+
+    t0 = time.perf_counter()
+    th = threading.Thread(target=serve)
+    th.start()
+    for _ in range(reps):
+        out["pt"] = open_wire(_recv_exact(client, wire_len))
+    th.join()
+    dt = time.perf_counter() - t0
+    server.close()
+    client.close()
+    return dt, out["pt"]
+
+
+def run_cpu(body, reps):
+    import oracle as ora
+
+    rc, key, iv = ora.key_from_secret(32, SECRET, 16, 12)
+    assert rc == 0
+    frags = [body[i * CONTENT:(i + 1) * CONTENT] for i in range(N_REC)]
+
+    def seal_body():
+        parts = []
+        for seq, f in enumerate(frags):
+            rc, wire = ora.record_seal(0x1301, key, iv, seq, 23, f)
+            assert rc == 0
+            parts.append(wire)
+        return b"".join(parts)
+
+    def open_wire(wire):
+        pt, pos = [], 0
+        for seq in range(N_REC):
+            n = (wire[pos + 3] << 8) | wire[pos + 4]
+            rc, frag, ctype = ora.record_open(0x1301, key, iv, seq, wire[pos:pos + 5 + n])
+            assert rc == 0 and ctype == 23
+            pt.append(frag)
+            pos += 5 + n
+        return b"".join(pt)
+
+    wire_len = N_REC * (5 + CONTENT + 1 + 16)
+    return _loop(seal_body, open_wire, wire_len, reps)
+
+
+def run_gpu(body, reps):
+    import anothertls_amd as atls
+    from anothertls_amd import record
+
+    eng = atls.Engine(0)
+    keys = eng.derive_keys(0x1301, SECRET)  # one connection: the server's write key
+    eng.set_keys(keys)
+    recs = np.zeros(N_REC, atls.REC_DTYPE)
+    recs["in_off"] = np.arange(N_REC) * CONTENT
+    recs["out_off"] = np.arange(N_REC) * (CONTENT + 16)  # round16(content + type)
+    recs["len"] = CONTENT
+    recs["seq"] = np.arange(N_REC)
+    recs["content_type"] = 23
+    recs["mode"] = atls.MODE_TLS
+    inbuf = np.frombuffer(body, np.uint8)
+    out = np.zeros(N_REC * (CONTENT + 16), np.uint8)
+    tags = np.zeros(16 * N_REC, np.uint8)
+    aux = np.zeros(16, np.uint8)
+    wire_len = N_REC * (5 + CONTENT + 1 + 16)
+
+    def seal_body():
+        eng.seal_batch(recs, inbuf, aux, out, tags)
+        return record.frame_sealed(recs, out, tags).tobytes()
+
+    def open_wire(wire):
+        w = np.frombuffer(wire, np.uint8)
+        offs, lens = record.parse_stream(w)
+        orecs = np.zeros(len(offs), atls.REC_DTYPE)
+        orecs["in_off"] = offs + 5
+        orecs["out_off"] = offs + 5
+        orecs["len"] = lens - 16
+        orecs["seq"] = np.arange(len(offs))
+        orecs["mode"] = atls.MODE_TLS
+        itags = np.concatenate([w[o + 5 + n - 16:o + 5 + n] for o, n in zip(offs, lens)])
+        pt = np.zeros_like(w)
+        res = np.zeros(len(offs), atls.OPEN_RESULT_DTYPE)
+        eng.open_batch(orecs, w, aux, itags, pt, res)
+        assert (res["status"] == 0).all() and (res["content_type"] == 23).all(), res
+        return b"".join(pt[o + 5:o + 5 + int(c)].tobytes() for o, c in zip(offs, res["content_len"]))
+
+    _loop(seal_body, open_wire, wire_len, 1)  # warm-up (device buffers, code objects)
+    dt, pt = _loop(seal_body, open_wire, wire_len, reps)
+    eng.close()
+    return dt, pt
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--reps", type=int, default=8)
+    p.add_argument("--cpu-reps", type=int, default=1)
+    p.add_argument("--cpu-only", action="store_true")
+    args = p.parse_args()
+    body = np.random.default_rng(0xC1).integers(0, 256, N_REC * CONTENT, dtype=np.uint8).tobytes()
+    res = {"config": "c1_server_https_loopback_1MiB", "records": N_REC, "suite": "TLS_AES_128_GCM_SHA256",
+           "body_bytes": len(body)}
+    dt, pt = run_cpu(body, args.cpu_reps)
+    assert pt == body
+    res["cpu_reference_MBps"] = round(args.cpu_reps * len(body) / dt / 1e6, 3)
+    if not args.cpu_only:
+        dt, pt = run_gpu(body, args.reps)
+        assert pt == body
+        res["gpu_MBps"] = round(args.reps * len(body) / dt / 1e6, 1)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
