@@ -74,6 +74,7 @@ struct atls_engine {
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
   DevBuf plan, plan_keys, plan_idx;          // batch plan (plan.hip)
   bool force_plan = false;                   // ATLS_FORCE_PLAN=1: plan every batch (tests)
+  bool no_pipeline = false;                  // ATLS_NO_PIPELINE=1: stage host batches in one piece
   std::mutex mu;
 };
 
@@ -104,6 +105,93 @@ void extents(const atls_rec* recs, uint32_t n, bool open, size_t* in_end, size_t
   *aux_end = c;
 }
 
+int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n, const uint8_t* d_in,
+                   const uint8_t* d_aux, uint8_t* d_out, uint8_t* d_tags_out, const uint8_t* d_tags_in,
+                   atls_open_result* d_res, hipStream_t s) {
+  // direct batches only (one record kernel in the key table)
+  if (e->has_chacha)
+    return atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, nullptr,
+                              e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * 8, s);
+  return atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
+                         (const uint32_t*)e->t0.p, nullptr, e->plan.p, (uint32_t*)e->err.p, e->n_slots,
+                         e->aes_nr_mask, e->cus, s);
+}
+
+// Host-memory batch (the socket path) in record chunks of ~kChunkBytes, alternating between the
+// engine's two streams: chunk c+1's host-to-device copy overlaps chunk c's kernel and its
+// device-to-host copy (separate DMA engines; full speed with pinned host buffers). Needs records
+// whose input and output ranges increase with the record index. When every record has the same
+// output length and the outputs sit at a fixed pitch, only record bytes travel back
+// (hipMemcpy2DAsync), so the bytes of `out` between records need not be staged in: they stay as
+// the caller had them. Otherwise each chunk's whole output range is staged in and copied back.
+// Returns -1 when the batch does not qualify (the caller then stages the batch in one piece).
+int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
+                       void* out, uint8_t* tags_out, const uint8_t* tags_in, atls_open_result* res,
+                       size_t in_end, size_t out_end, size_t aux_end) {
+  constexpr size_t kChunkBytes = 32u << 20;
+  auto olen = [&](const atls_rec& r) { return (r.mode == ATLS_MODE_TLS && !open) ? (size_t)r.len + 1 : (size_t)r.len; };
+  for (uint32_t i = 1; i < n; i++)
+    if (recs[i].in_off < recs[i - 1].in_off + recs[i - 1].len || recs[i].out_off < recs[i - 1].out_off + olen(recs[i - 1]))
+      return -1;
+  bool pitched = n > 1;
+  const size_t pitch = n > 1 ? (size_t)(recs[1].out_off - recs[0].out_off) : 0, width = olen(recs[0]);
+  for (uint32_t i = 1; i < n && pitched; i++)
+    pitched = olen(recs[i]) == width && recs[i].out_off == recs[0].out_off + i * pitch;
+  hipStream_t st[2] = {e->stream, e->stream2};
+  hipEvent_t ev[2] = {e->ev_plan, e->ev_side};
+  // descriptors, aux and err are in place (stream 0) before the other stream starts
+  if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, st[0]) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  if (hipMemsetAsync(e->err.p, 0, 4, st[0]) != hipSuccess || hipEventRecord(ev[0], st[0]) != hipSuccess ||
+      hipStreamWaitEvent(st[1], ev[0], 0) != hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  const auto* d_recs = (const atls_rec*)e->recs.p;
+  auto* d_in = (uint8_t*)e->in.p;
+  auto* d_out = (uint8_t*)e->out.p;
+  auto* d_tags = (uint8_t*)e->tags.p;
+  auto* d_res = (atls_open_result*)e->res.p;
+  (void)in_end;
+  (void)out_end;
+  int c = 0;
+  for (uint32_t a = 0; a < n; c ^= 1) {
+    uint32_t b = a + 1;
+    while (b < n && recs[b - 1].in_off + recs[b - 1].len - recs[a].in_off < kChunkBytes) b++;
+    hipStream_t s = st[c];
+    const size_t in_lo = recs[a].in_off, in_hi = recs[b - 1].in_off + recs[b - 1].len;
+    const size_t out_lo = recs[a].out_off, out_hi = recs[b - 1].out_off + olen(recs[b - 1]);
+    const uint32_t cnt = b - a;
+    if (in_hi > in_lo &&
+        hipMemcpyAsync(d_in + in_lo, (const uint8_t*)in + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    if (open && hipMemcpyAsync(d_tags + 16 * (size_t)a, tags_in + 16 * (size_t)a, 16 * (size_t)cnt,
+                               hipMemcpyHostToDevice, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    if (!pitched && out_hi > out_lo &&
+        hipMemcpyAsync(d_out + out_lo, (uint8_t*)out + out_lo, out_hi - out_lo, hipMemcpyHostToDevice, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    int rc = launch_records(e, open, d_recs + a, cnt, d_in, (const uint8_t*)e->aux.p, d_out, d_tags + 16 * (size_t)a,
+                            d_tags + 16 * (size_t)a, d_res + a, s);
+    if (rc) return rc;
+    if (pitched) {
+      if (width && hipMemcpy2DAsync((uint8_t*)out + out_lo, pitch, d_out + out_lo, pitch, width, cnt,
+                                    hipMemcpyDeviceToHost, s) != hipSuccess)
+        return ATLS_INTERNAL_ERROR;
+    } else if (out_hi > out_lo &&
+               hipMemcpyAsync((uint8_t*)out + out_lo, d_out + out_lo, out_hi - out_lo, hipMemcpyDeviceToHost, s) != hipSuccess) {
+      return ATLS_INTERNAL_ERROR;
+    }
+    if (!open && hipMemcpyAsync(tags_out + 16 * (size_t)a, d_tags + 16 * (size_t)a, 16 * (size_t)cnt,
+                                hipMemcpyDeviceToHost, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    if (open && hipMemcpyAsync(res + a, d_res + a, sizeof(atls_open_result) * (size_t)cnt, hipMemcpyDeviceToHost, s) !=
+                    hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    a = b;
+  }
+  if (hipEventRecord(ev[1], st[1]) != hipSuccess || hipStreamWaitEvent(st[0], ev[1], 0) != hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  return finish(e, 0);
+}
+
 int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
               void* out, uint8_t* tags_out, const uint8_t* tags_in, atls_open_result* res, uint32_t flags) {
   if (!e) return ATLS_INTERNAL_ERROR;
@@ -132,11 +220,20 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   const uint8_t* d_tags_in = tags_in;
   atls_open_result* d_res = res;
   size_t in_end = 0, out_end = 0, aux_end = 0;
+  // A key table holding one record kernel's suite and round count gives a direct batch: that
+  // kernel walks the descriptors itself. Otherwise the batch is planned (plan.hip): ~30 us of
+  // small launches that sort records into per-kernel lists, longest first.
+  const int kinds = (e->has_chacha ? 1 : 0) + __builtin_popcount((unsigned)e->aes_nr_mask);
+  const bool planned = kinds > 1 || e->force_plan;
   if (!dev_ptrs) {
     extents(recs, n, open, &in_end, &out_end, &aux_end);
     if (!e->in.reserve(in_end + 16) || !e->out.reserve(out_end + 16) || !e->aux.reserve(aux_end + 16) ||
         !e->tags.reserve(16 * (size_t)n) || !e->res.reserve(sizeof(atls_open_result) * (size_t)n))
       return ATLS_INTERNAL_ERROR;
+    if (!planned && n > 1 && !e->no_pipeline) {
+      const int rc = run_host_pipelined(e, open, recs, n, in, aux, out, tags_out, tags_in, res, in_end, out_end, aux_end);
+      if (rc != -1) return rc;
+    }
     if (in_end && hipMemcpyAsync(e->in.p, in, in_end, hipMemcpyHostToDevice, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
     if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
@@ -154,11 +251,6 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   }
   if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
   int rc = 0;
-  // A key table holding one record kernel's suite and round count gives a direct batch: that
-  // kernel walks the descriptors itself. Otherwise the batch is planned (plan.hip): ~30 us of
-  // small launches that sort records into per-kernel lists, longest first.
-  const int kinds = (e->has_chacha ? 1 : 0) + __builtin_popcount((unsigned)e->aes_nr_mask);
-  const bool planned = kinds > 1 || e->force_plan;
   const uint32_t* idx = nullptr;
   if (planned) {
     if (!e->plan.reserve(sizeof(atls::PlanHdr)) || !e->plan_keys.reserve(n) || !e->plan_idx.reserve(4 * (size_t)n))
@@ -309,6 +401,7 @@ atls_engine* atls_engine_create(int device) {
   }
   e->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   if (const char* v = std::getenv("ATLS_FORCE_PLAN")) e->force_plan = std::atoi(v) != 0;
+  if (const char* v = std::getenv("ATLS_NO_PIPELINE")) e->no_pipeline = std::atoi(v) != 0;
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
       hipStreamSynchronize(e->stream) != hipSuccess) {
     atls_engine_destroy(e);

@@ -174,9 +174,13 @@ def main():
             h_in = d_in[: int(recs["in_off"][sample - 1]) + int(recs["len"][sample - 1]) + 16].cpu().numpy()
             result["cpu_baseline"] = cpu_baseline(batch, h_in, args.cpu_seconds, args.cpu_threads)
         if args.pcie and world == 1:
-            h_in = d_in.cpu().numpy()
-            h_out = np.empty(batch["out_bytes"], np.uint8)
-            h_tags = np.empty(16 * n, np.uint8)
+            # host-memory batches (the socket path): the engine stages them over PCIe; pinned
+            # (page-locked) host buffers as a record layer would keep its socket buffers in
+            def pinned(nbytes):
+                return torch.empty(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
+
+            h_in, h_out, h_tags = pinned(batch["in_bytes"]), pinned(batch["out_bytes"]), pinned(16 * n)
+            h_in[:] = d_in.cpu().numpy()
             eng.seal_batch(recs, h_in, np.zeros(16, np.uint8), h_out, h_tags)
             t0 = time.perf_counter()
             for _ in range(3):
