@@ -93,7 +93,7 @@ OPEN_RESULT_DTYPE = np.dtype([("content_len", "<u4"), ("status", "u1"), ("conten
                               ("reserved", "u1", 2)])
 assert KEY_DTYPE.itemsize == 64 and REC_DTYPE.itemsize == 48 and OPEN_RESULT_DTYPE.itemsize == 8
 
-MODE_TLS, MODE_RAW = 0, 1
+MODE_TLS, MODE_RAW, MODE_WIRE = 0, 1, 2
 FLAG_DEVICE_PTRS, FLAG_DEVICE_RECS, FLAG_NO_SYNC = 1, 2, 4
 
 

@@ -37,6 +37,31 @@ __host__ __device__ inline uint32_t bswap32(uint32_t x) {
 }
 __host__ __device__ inline uint32_t rotl32(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 
+// 16-byte global load / store at any byte address. The amdhsa ABI runs gfx9+ with unaligned
+// access enabled, so these compile to one global_load/store_dwordx4 whatever the alignment:
+// records at any offset (wire records put the ciphertext 5 bytes past the header) keep the
+// vector path.
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);
+  return v;
+}
+__device__ __forceinline__ void st16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
+
+// RecordType::new (net/record.rs:22-33): Invalid(0), ChangeCipherSpec, Alert, Handshake,
+// ApplicationData.
+__host__ __device__ inline bool record_type_ok(uint32_t b) { return b == 0 || (b >= 20 && b <= 23); }
+
+// ATLS_MODE_WIRE open: the 5 received header bytes at p (the record's AAD, record.rs:219) as
+// raw little-endian words, and whether they frame a record of len ciphertext bytes + 16 B tag
+// (Record::from_raw, record.rs:81-102).
+__device__ __forceinline__ bool wire_header(const uint8_t* p, uint32_t len, uint32_t& hdr0, uint32_t& hdr1) {
+  const uint32_t b0 = p[0], b1 = p[1], b2 = p[2], b3 = p[3], b4 = p[4];
+  hdr0 = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+  hdr1 = b4;
+  return record_type_ok(b0) && ((b3 << 8) | b4) == len + 16u;
+}
+
 // GF(2^128) multiply by x in the reference's bit order (be words): right shift, reduce by 0xE1.
 __host__ __device__ inline void gf_mulx_be(uint32_t v[4]) {
   uint32_t lsb = v[3] & 1u;

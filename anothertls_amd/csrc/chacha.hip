@@ -135,26 +135,32 @@ struct ChArgs {
 
 template <bool OPEN>
 __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl) {
-  const bool tls = d.mode == ATLS_MODE_TLS;
+  // TLS and WIRE: nonce from (static IV, seq), 5-byte AAD; WIRE also frames the record
+  const bool wire = d.mode == ATLS_MODE_WIRE;
+  const bool tls = d.mode != ATLS_MODE_RAW;
   const uint32_t len = d.len;
   const uint32_t n = (tls && !OPEN) ? len + 1 : len;
-  const uint8_t* src = A.in + d.in_off;
-  uint8_t* dst = A.out + d.out_off;
-  const bool src_al = ((reinterpret_cast<uintptr_t>(src)) & 15u) == 0;
-  const bool dst_al = ((reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+  const uint8_t* rec_in = A.in + d.in_off;
+  const uint8_t* src = rec_in + ((OPEN && wire) ? 5u : 0u);
+  uint8_t* dst = A.out + d.out_off + ((!OPEN && wire) ? 5u : 0u);
 
   uint32_t kw[8];
   for (int i = 0; i < 8; i++) kw[i] = k->kw[i];
   uint32_t nw[3];
   uint32_t aad_len = 5, hdr0 = 0, hdr1 = 0;
   const uint8_t* aadp = nullptr;
+  bool hdr_ok = true;
   if (tls) {
     nw[0] = k->siv[0];
     nw[1] = k->siv[1] ^ bswap32((uint32_t)(d.seq >> 32));
     nw[2] = k->siv[2] ^ bswap32((uint32_t)d.seq);
-    const uint32_t L = n + 16;
-    hdr0 = 0x17u | (0x03u << 8) | (0x03u << 16) | (((L >> 8) & 0xffu) << 24);
-    hdr1 = L & 0xffu;
+    if (OPEN && wire) {  // the received header is the AAD (record.rs:219)
+      hdr_ok = wire_header(rec_in, len, hdr0, hdr1);
+    } else {
+      const uint32_t L = n + 16;
+      hdr0 = 0x17u | (0x03u << 8) | (0x03u << 16) | (((L >> 8) & 0xffu) << 24);
+      hdr1 = L & 0xffu;
+    }
   } else {
     const uint8_t* iv = A.aux + d.aux_off;
     for (int w = 0; w < 3; w++)
@@ -229,11 +235,10 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         const uint32_t off = 64u * (j - 1);
         uint32_t P[16];
         const uint32_t valid = min(64u, n - off);
-        if (off + 64 <= len && src_al) {
-          const uint4* s4 = reinterpret_cast<const uint4*>(src + off);
+        if (off + 64 <= len) {
 #pragma unroll
           for (int q = 0; q < 4; q++) {
-            const uint4 v = s4[q];
+            const uint4 v = ld16(src + off + 16 * q);
             P[4 * q] = v.x; P[4 * q + 1] = v.y; P[4 * q + 2] = v.z; P[4 * q + 3] = v.w;
           }
         } else {
@@ -257,10 +262,9 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
             if ((int)valid < lo + 4) C[q] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - (int)valid)));
           }
         }
-        if (valid == 64 && dst_al) {
-          uint4* d4 = reinterpret_cast<uint4*>(dst + off);
+        if (valid == 64) {
 #pragma unroll
-          for (int q = 0; q < 4; q++) d4[q] = make_uint4(C[4 * q], C[4 * q + 1], C[4 * q + 2], C[4 * q + 3]);
+          for (int q = 0; q < 4; q++) st16(dst + off + 16 * q, make_uint4(C[4 * q], C[4 * q + 1], C[4 * q + 2], C[4 * q + 3]));
         } else {
 #pragma unroll
           for (int q = 0; q < 64; q++)
@@ -342,8 +346,14 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 
   if (!OPEN) {
     if (gl == 0) {
-      uint32_t* tg = reinterpret_cast<uint32_t*>(A.tags_out + 16ull * rec_idx);
-      tg[0] = tag[0]; tg[1] = tag[1]; tg[2] = tag[2]; tg[3] = tag[3];
+      const uint4 t = make_uint4(tag[0], tag[1], tag[2], tag[3]);
+      if (A.tags_out) st16(A.tags_out + 16ull * rec_idx, t);
+      if (wire) {  // header || ciphertext || tag (record.rs:175-197)
+        uint8_t* h = dst - 5;
+        h[0] = (uint8_t)hdr0; h[1] = (uint8_t)(hdr0 >> 8); h[2] = (uint8_t)(hdr0 >> 16);
+        h[3] = (uint8_t)(hdr0 >> 24); h[4] = (uint8_t)hdr1;
+        st16(dst + n, t);
+      }
     }
   } else {
     for (int off = G / 2; off >= 1; off >>= 1) {
@@ -351,11 +361,15 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       lastnz = o > lastnz ? o : lastnz;
     }
     if (gl == 0) {
-      const uint32_t* tg = reinterpret_cast<const uint32_t*>(A.tags_in + 16ull * rec_idx);
-      const bool ok = (tg[0] == tag[0]) & (tg[1] == tag[1]) & (tg[2] == tag[2]) & (tg[3] == tag[3]);
+      const uint4 tg = ld16(wire ? src + len : A.tags_in + 16ull * rec_idx);  // WIRE: tag follows the ct
+      const bool ok = (tg.x == tag[0]) & (tg.y == tag[1]) & (tg.z == tag[2]) & (tg.w == tag[3]);
       atls_open_result rr;
       rr.reserved[0] = rr.reserved[1] = 0;
-      if (!tls) {
+      if (!hdr_ok) {  // WIRE: the header does not frame this record (record.rs:81-102)
+        rr.status = ATLS_DECODE_ERROR;
+        rr.content_len = 0;
+        rr.content_type = 0;
+      } else if (!tls) {
         rr.status = ok ? ATLS_OK : ATLS_BAD_RECORD_MAC;
         rr.content_len = len;
         rr.content_type = 0;

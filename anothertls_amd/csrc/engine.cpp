@@ -90,14 +90,23 @@ int finish(atls_engine* e, uint32_t flags) {
   return err ? ATLS_ILLEGAL_PARAMETER : ATLS_OK;
 }
 
+// Bytes a record reads at in_off and writes at out_off. TLS seal: content + type byte out;
+// WIRE seal: header || ct || tag out; WIRE open: header || ct || tag in.
+size_t rec_in_len(const atls_rec& r, bool open) {
+  return (r.mode == ATLS_MODE_WIRE && open) ? (size_t)r.len + 21 : (size_t)r.len;
+}
+size_t rec_out_len(const atls_rec& r, bool open) {
+  if (open || r.mode == ATLS_MODE_RAW) return r.len;
+  return r.mode == ATLS_MODE_WIRE ? (size_t)r.len + 22 : (size_t)r.len + 1;
+}
+
 // Largest byte extent touched by the descriptors (host-memory mode only).
 void extents(const atls_rec* recs, uint32_t n, bool open, size_t* in_end, size_t* out_end, size_t* aux_end) {
   size_t a = 0, b = 0, c = 0;
   for (uint32_t i = 0; i < n; i++) {
     const atls_rec& r = recs[i];
-    const size_t outlen = (r.mode == ATLS_MODE_TLS && !open) ? (size_t)r.len + 1 : r.len;
-    a = std::max(a, (size_t)r.in_off + r.len);
-    b = std::max(b, (size_t)r.out_off + outlen);
+    a = std::max(a, (size_t)r.in_off + rec_in_len(r, open));
+    b = std::max(b, (size_t)r.out_off + rec_out_len(r, open));
     if (r.mode == ATLS_MODE_RAW) c = std::max(c, (size_t)r.aux_off + r.iv_len + r.aad_len);
   }
   *in_end = a;
@@ -129,9 +138,10 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
                        void* out, uint8_t* tags_out, const uint8_t* tags_in, atls_open_result* res,
                        size_t in_end, size_t out_end, size_t aux_end) {
   constexpr size_t kChunkBytes = 32u << 20;
-  auto olen = [&](const atls_rec& r) { return (r.mode == ATLS_MODE_TLS && !open) ? (size_t)r.len + 1 : (size_t)r.len; };
+  auto ilen = [&](const atls_rec& r) { return rec_in_len(r, open); };
+  auto olen = [&](const atls_rec& r) { return rec_out_len(r, open); };
   for (uint32_t i = 1; i < n; i++)
-    if (recs[i].in_off < recs[i - 1].in_off + recs[i - 1].len || recs[i].out_off < recs[i - 1].out_off + olen(recs[i - 1]))
+    if (recs[i].in_off < recs[i - 1].in_off + ilen(recs[i - 1]) || recs[i].out_off < recs[i - 1].out_off + olen(recs[i - 1]))
       return -1;
   bool pitched = n > 1;
   const size_t pitch = n > 1 ? (size_t)(recs[1].out_off - recs[0].out_off) : 0, width = olen(recs[0]);
@@ -154,15 +164,15 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   int c = 0;
   for (uint32_t a = 0; a < n; c ^= 1) {
     uint32_t b = a + 1;
-    while (b < n && recs[b - 1].in_off + recs[b - 1].len - recs[a].in_off < kChunkBytes) b++;
+    while (b < n && recs[b - 1].in_off + ilen(recs[b - 1]) - recs[a].in_off < kChunkBytes) b++;
     hipStream_t s = st[c];
-    const size_t in_lo = recs[a].in_off, in_hi = recs[b - 1].in_off + recs[b - 1].len;
+    const size_t in_lo = recs[a].in_off, in_hi = recs[b - 1].in_off + ilen(recs[b - 1]);
     const size_t out_lo = recs[a].out_off, out_hi = recs[b - 1].out_off + olen(recs[b - 1]);
     const uint32_t cnt = b - a;
     if (in_hi > in_lo &&
         hipMemcpyAsync(d_in + in_lo, (const uint8_t*)in + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
-    if (open && hipMemcpyAsync(d_tags + 16 * (size_t)a, tags_in + 16 * (size_t)a, 16 * (size_t)cnt,
+    if (open && tags_in && hipMemcpyAsync(d_tags + 16 * (size_t)a, tags_in + 16 * (size_t)a, 16 * (size_t)cnt,
                                hipMemcpyHostToDevice, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     if (!pitched && out_hi > out_lo &&
@@ -179,7 +189,7 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
                hipMemcpyAsync((uint8_t*)out + out_lo, d_out + out_lo, out_hi - out_lo, hipMemcpyDeviceToHost, s) != hipSuccess) {
       return ATLS_INTERNAL_ERROR;
     }
-    if (!open && hipMemcpyAsync(tags_out + 16 * (size_t)a, d_tags + 16 * (size_t)a, 16 * (size_t)cnt,
+    if (!open && tags_out && hipMemcpyAsync(tags_out + 16 * (size_t)a, d_tags + 16 * (size_t)a, 16 * (size_t)cnt,
                                 hipMemcpyDeviceToHost, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     if (open && hipMemcpyAsync(res + a, d_res + a, sizeof(atls_open_result) * (size_t)cnt, hipMemcpyDeviceToHost, s) !=
@@ -204,10 +214,16 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   const bool dev_recs = flags & ATLS_FLAG_DEVICE_RECS;
   if (!dev_ptrs && dev_recs) return ATLS_ILLEGAL_PARAMETER;  // host buffers need host-visible descriptors
 
+  // No tags array: every record must carry its tag in the wire record (ATLS_MODE_WIRE). The
+  // kernels then get the engine's scratch array, so a device-resident non-WIRE descriptor cannot
+  // fault (it seals into scratch, or fails authentication on open).
+  const bool no_tags = open ? !tags_in : !tags_out;
+  if (no_tags && !e->tags.reserve(16 * (size_t)n)) return ATLS_INTERNAL_ERROR;
   const atls_rec* d_recs = recs;
   if (!dev_recs) {
     for (uint32_t i = 0; i < n; i++)
-      if (recs[i].key_slot >= e->n_slots || recs[i].mode > ATLS_MODE_RAW) return ATLS_ILLEGAL_PARAMETER;
+      if (recs[i].key_slot >= e->n_slots || recs[i].mode > ATLS_MODE_WIRE || (no_tags && recs[i].mode != ATLS_MODE_WIRE))
+        return ATLS_ILLEGAL_PARAMETER;
     if (!e->recs.reserve(sizeof(atls_rec) * (size_t)n)) return ATLS_INTERNAL_ERROR;
     if (hipMemcpyAsync(e->recs.p, recs, sizeof(atls_rec) * (size_t)n, hipMemcpyHostToDevice, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
@@ -216,8 +232,8 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   const uint8_t* d_in = (const uint8_t*)in;
   const uint8_t* d_aux = (const uint8_t*)aux;
   uint8_t* d_out = (uint8_t*)out;
-  uint8_t* d_tags_out = tags_out;
-  const uint8_t* d_tags_in = tags_in;
+  uint8_t* d_tags_out = no_tags ? (uint8_t*)e->tags.p : tags_out;
+  const uint8_t* d_tags_in = no_tags ? (const uint8_t*)e->tags.p : tags_in;
   atls_open_result* d_res = res;
   size_t in_end = 0, out_end = 0, aux_end = 0;
   // A key table holding one record kernel's suite and round count gives a direct batch: that
@@ -237,7 +253,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     if (in_end && hipMemcpyAsync(e->in.p, in, in_end, hipMemcpyHostToDevice, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
     if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
-    if (open && hipMemcpyAsync(e->tags.p, tags_in, 16 * (size_t)n, hipMemcpyHostToDevice, s) != hipSuccess)
+    if (open && tags_in && hipMemcpyAsync(e->tags.p, tags_in, 16 * (size_t)n, hipMemcpyHostToDevice, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     // Bytes of `out` outside the records must come back unchanged: stage them in too.
     if (out_end && hipMemcpyAsync(e->out.p, out, out_end, hipMemcpyHostToDevice, s) != hipSuccess)
@@ -284,7 +300,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   if (!dev_ptrs) {
     if (out_end && hipMemcpyAsync(out, e->out.p, out_end, hipMemcpyDeviceToHost, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
-    if (!open && hipMemcpyAsync(tags_out, e->tags.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess)
+    if (!open && tags_out && hipMemcpyAsync(tags_out, e->tags.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     if (open && hipMemcpyAsync(res, e->res.p, sizeof(atls_open_result) * (size_t)n, hipMemcpyDeviceToHost, s) !=
                     hipSuccess)

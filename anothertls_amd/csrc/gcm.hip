@@ -185,20 +185,25 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     rk[i] = cptr(k->rk)[i];  // wave-uniform: scalar loads
     rkr[i] = cptr(k->rkr)[i];
   }
-  const bool tls = d.mode == ATLS_MODE_TLS;
+  // TLS and WIRE: nonce from (static IV, seq), one AAD block; WIRE also frames the record
+  const bool wire = d.mode == ATLS_MODE_WIRE;
+  const bool tls = d.mode != ATLS_MODE_RAW;
   const uint32_t len = d.len;
   const uint32_t n_aead = (tls && !OPEN) ? len + 1 : len;  // record.rs:172-173 inner plaintext
-  const uint8_t* src = A.in + d.in_off;
-  uint8_t* dst = A.out + d.out_off;
+  const uint8_t* rec_in = A.in + d.in_off;
+  const uint8_t* src = rec_in + ((OPEN && wire) ? 5u : 0u);
+  uint8_t* dst = A.out + d.out_off + ((!OPEN && wire) ? 5u : 0u);
+  // Unaligned records (wire framing) keep the vector fast steps (ld16/st16); the few general
+  // steps go bytewise for them (vector accesses there cost registers the seal kernel lacks).
   const bool src_al = ((reinterpret_cast<uintptr_t>(src)) & 15u) == 0;
   const bool dst_al = ((reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
-
   // ---- nonce / J0 (gcm.rs:59-74) and AAD ----
   uint32_t j0[4];  // be words
   bool is96 = true;
   uint32_t hdr0 = 0, hdr1 = 0;  // TLS AAD header, raw words
   const uint8_t* aadp = nullptr;
   uint32_t aad_len = 5;
+  bool hdr_ok = true;
   if (tls) {
     // key_schedule.rs:51-64: nonce = iv ^ (0^4 || be64(seq)); J0 = nonce || 0x00000001.
     const uint64_t seq = d.seq;
@@ -206,9 +211,13 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     j0[1] = bswap32(k->siv[1]) ^ (uint32_t)(seq >> 32);
     j0[2] = bswap32(k->siv[2]) ^ (uint32_t)seq;
     j0[3] = 1u;
-    const uint32_t L = n_aead + 16;  // record.rs:176-183, truncated to 16 bits
-    hdr0 = 0x17u | (0x03u << 8) | (0x03u << 16) | (((L >> 8) & 0xffu) << 24);
-    hdr1 = L & 0xffu;
+    if (OPEN && wire) {  // the received header is the AAD (record.rs:219)
+      hdr_ok = wire_header(rec_in, len, hdr0, hdr1);
+    } else {
+      const uint32_t L = n_aead + 16;  // record.rs:176-183, truncated to 16 bits
+      hdr0 = 0x17u | (0x03u << 8) | (0x03u << 16) | (((L >> 8) & 0xffu) << 24);
+      hdr1 = L & 0xffu;
+    }
   } else {
     const uint8_t* iv = A.aux + d.aux_off;
     const uint32_t iv_len = d.iv_len;
@@ -255,11 +264,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   uint32_t y[4] = {0, 0, 0, 0};
   uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0), lane 0
   int64_t lastnz = -1;                      // OPEN+TLS: (pos << 8 | byte) of last non-zero pt byte
-  const bool fast_src = src_al, fast_dst = dst_al;
   // Slots [64, fast_end) are full 16-byte data blocks that lie wholly inside the input and
   // output: for them the step below runs branch-free (no classification, no partial handling).
   const uint32_t full_blocks = min(in_bytes, n_aead) / 16u;
-  const uint32_t fast_end = (src_al && dst_al && is96) ? na + 1u + full_blocks : 0u;
+  const uint32_t fast_end = is96 ? na + 1u + full_blocks : 0u;
 
   // Counter cache (CtrCache): every 64-slot step's counters share ctr >> 8 when the counter of slot
   // `base` is a multiple of 64 -- records with one AAD block (all TLS records) and a 96-bit IV.
@@ -294,7 +302,8 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     const uint32_t s = base + (uint32_t)lane;
     if (base >= 64u && base + 64u <= fast_end) {  // wave-uniform
       const uint32_t off = (s - 1u - na) * 16u;
-      const v4u32 P = *reinterpret_cast<const v4u32*>(src + off);
+      const uint4 Pu = ld16(src + off);
+      const v4u32 P = {Pu.x, Pu.y, Pu.z, Pu.w};
       uint32_t st[4];
       if (use_cache) {
         const uint32_t c0 = j0[3] + base - na;  // counter of lane 0, a multiple of 64
@@ -305,7 +314,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
         aes_encrypt_tt<NR>(st, rk, rkr, lb);
       }
       const v4u32 C = {P.x ^ st[0], P.y ^ st[1], P.z ^ st[2], P.w ^ st[3]};
-      *reinterpret_cast<v4u32*>(dst + off) = C;
+      st16(dst + off, make_uint4(C.x, C.y, C.z, C.w));
       const v4u32 Bv = OPEN ? P : C;
       if (OPEN && tls) {
         const uint32_t cw[4] = {C.x, C.y, C.z, C.w};
@@ -340,7 +349,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     const uint32_t g = s - 1;
     if (s >= 1 && s <= m && g >= na && g < na + nb) {
       const uint32_t off = (g - na) * 16;
-      if (off + 16 <= in_bytes && fast_src) {
+      if (off + 16 <= in_bytes && src_al) {
         const uint4 v = *reinterpret_cast<const uint4*>(src + off);
         P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
       } else {
@@ -384,7 +393,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
             if ((int)valid < lo + 4) C[w] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
           }
         }
-        if (valid == 16 && fast_dst) {
+        if (valid == 16 && dst_al) {
           *reinterpret_cast<uint4*>(dst + off) = make_uint4(C[0], C[1], C[2], C[3]);
         } else {
 #pragma unroll
@@ -437,8 +446,13 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 
   if (!OPEN) {
     if (lane == 0) {
-      uint32_t* tg = reinterpret_cast<uint32_t*>(A.tags_out + 16ull * rec_idx);
-      tg[0] = t0; tg[1] = t1; tg[2] = t2; tg[3] = t3;
+      if (A.tags_out) st16(A.tags_out + 16ull * rec_idx, make_uint4(t0, t1, t2, t3));
+      if (wire) {  // header || ciphertext || tag (record.rs:175-197)
+        uint8_t* h = dst - 5;
+        h[0] = (uint8_t)hdr0; h[1] = (uint8_t)(hdr0 >> 8); h[2] = (uint8_t)(hdr0 >> 16);
+        h[3] = (uint8_t)(hdr0 >> 24); h[4] = (uint8_t)hdr1;
+        st16(dst + n_aead, make_uint4(t0, t1, t2, t3));
+      }
     }
   } else {
     // content-type scan (record.rs:229-237): wave max of (pos << 8 | byte)
@@ -448,9 +462,9 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       lastnz = o > lastnz ? o : lastnz;
     }
     if (lane == 0) {
-      const uint32_t* tg = reinterpret_cast<const uint32_t*>(A.tags_in + 16ull * rec_idx);
-      const bool ok = (tg[0] == t0) & (tg[1] == t1) & (tg[2] == t2) & (tg[3] == t3);
-      write_open_result(A, rec_idx, tls, len, ok, lastnz);
+      const uint4 tg = ld16(wire ? src + len : A.tags_in + 16ull * rec_idx);  // WIRE: tag follows the ct
+      const bool ok = (tg.x == t0) & (tg.y == t1) & (tg.z == t2) & (tg.w == t3);
+      write_open_result(A, rec_idx, tls, len, ok, lastnz, hdr_ok);
     }
   }
 #ifdef ATLS_TT_STAMPS

@@ -205,10 +205,14 @@ struct GcmArgs {
 // Open result for one record (record.rs:203-240 decrypt + padding scan). lastnz = (position <<
 // 8 | byte) of the last non-zero plaintext byte, -1 if none.
 __device__ __forceinline__ void write_open_result(const GcmArgs& A, uint32_t rec_idx, bool tls, uint32_t len, bool ok,
-                                                  int64_t lastnz) {
+                                                  int64_t lastnz, bool hdr_ok) {
   atls_open_result r;
   r.reserved[0] = r.reserved[1] = 0;
-  if (!tls) {
+  if (!hdr_ok) {  // WIRE: the header does not frame this record (record.rs:81-102)
+    r.status = ATLS_DECODE_ERROR;
+    r.content_len = 0;
+    r.content_type = 0;
+  } else if (!tls) {
     r.status = ok ? ATLS_OK : ATLS_BAD_RECORD_MAC;
     r.content_len = len;
     r.content_type = 0;

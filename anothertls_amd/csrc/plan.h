@@ -35,7 +35,7 @@ struct WorkList {
 // Direct mode: the status a record gets in place of sealing / opening (0 = process it), as
 // plan_key would give it (plan.hip).
 __device__ __forceinline__ uint32_t direct_reject(const atls_rec& d, const KeySched* ks, uint32_t n_slots) {
-  if (d.key_slot >= n_slots || d.mode > ATLS_MODE_RAW) return ATLS_ILLEGAL_PARAMETER;
+  if (d.key_slot >= n_slots || d.mode > ATLS_MODE_WIRE) return ATLS_ILLEGAL_PARAMETER;
   const KeySched* k = ks + d.key_slot;
   const uint32_t suite = k->suite;
   if (suite == (uint32_t)kSuiteChacha) return (!k->valid || (d.mode == ATLS_MODE_RAW && d.iv_len != 12)) ? ATLS_ILLEGAL_PARAMETER : 0;

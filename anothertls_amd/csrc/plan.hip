@@ -22,7 +22,7 @@ __device__ __forceinline__ uint32_t plan_key(const atls_rec* recs, uint32_t i, c
                                              uint8_t* st) {
   const atls_rec d = recs[i];
   *st = ATLS_ILLEGAL_PARAMETER;
-  if (d.key_slot >= n_slots || d.mode > ATLS_MODE_RAW) return kPlanReject;
+  if (d.key_slot >= n_slots || d.mode > ATLS_MODE_WIRE) return kPlanReject;
   const KeySched* k = ks + d.key_slot;
   const uint32_t suite = k->suite, valid = k->valid, nr = k->nr;
   uint32_t list;

@@ -9,7 +9,7 @@ records carry consecutive sequence numbers, as a record layer's writes would.
 """
 import numpy as np
 
-from . import KEY_DTYPE, MODE_TLS, REC_DTYPE, CipherSuite
+from . import KEY_DTYPE, MODE_TLS, MODE_WIRE, REC_DTYPE, CipherSuite
 
 SEEDS = {"payload": 0x5EED0001, "keys": 0x5EED0002, "layout": 0x5EED0003}
 
@@ -62,6 +62,28 @@ def tls_batch(n, lens, suites_per_key, n_keys=4096, content_type=23, seq_base=0,
                      np.full(n_keys, int(suites_per_key), dtype=np.uint16))
     return dict(keys=keys, recs=recs, in_bytes=int(in_sz.sum()) if n else 0,
                 out_bytes=int(out_sz.sum()) if n else 0, payload=int(lens.sum() + n))
+
+
+def wire_batch(b):
+    """The batch b with its records sealed as one contiguous wire stream (ATLS_MODE_WIRE): record
+    i's header || ciphertext || tag at out_off, 5 + len + 1 + 16 bytes, back to back as
+    RecordPayloadProtection::encrypt's outputs go on the socket (record.rs:162-198)."""
+    recs = b["recs"].copy()
+    wl = recs["len"].astype(np.uint64) + np.uint64(22)
+    recs["out_off"] = np.concatenate([[0], np.cumsum(wl)[:-1]]).astype(np.uint64) if len(recs) else []
+    recs["mode"] = MODE_WIRE
+    return dict(b, recs=recs, out_bytes=int(wl.sum()) if len(recs) else 0)
+
+
+def wire_open_descs(sealed):
+    """Open descriptors for a wire stream sealed with `sealed` (wire_batch records): each record
+    read at its wire offset with len = ciphertext bytes, plaintext out 16-byte aligned."""
+    recs = sealed.copy()
+    L = recs["len"].astype(np.uint64) + np.uint64(1)
+    recs["in_off"] = sealed["out_off"]
+    recs["len"] = L.astype(np.uint32)
+    recs["out_off"] = np.concatenate([[0], np.cumsum(_round16(L))[:-1]]).astype(np.uint64) if len(recs) else []
+    return recs, int(_round16(L).sum()) if len(recs) else 0
 
 
 def config_batch(name, n=None, first=0):

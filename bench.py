@@ -10,7 +10,11 @@ Fields beyond the driver contract:
   roofline     — dominant kernel (AES-GCM seal): algorithmic bytes per launch (2L+16 per record:
                  read L, write L ciphertext + 16 tag) / average launch time from HIP events on
                  the engine's stream; peak 8 TB/s HBM3E; traffic = PMC-measured HBM bytes per
-                 launch from profiles/ (null if not yet profiled).
+                 launch from profiles/ (null if not yet profiled); copy_GBps = a measured
+                 device-to-device copy of the payload buffer (read + write) and frac_of_copy =
+                 achieved / copy_GBps.
+  wire_GiBps   — (--wire) the same records sealed as one contiguous wire stream, header || ct ||
+                 tag per record (ATLS_MODE_WIRE), payload GiB/s from HIP events.
   cpu_baseline — the oracle (literal C restatement of the reference's algorithm: byte S-box
                  AES with bit-serial MixColumns, bit-serial GHASH) on a bounded sample of the
                  same records, on this host: --cpu-threads threads (value) and 1 thread
@@ -46,6 +50,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=16,
                    help="CPU-baseline threads (the GPU box's host share is 16 cores)")
     p.add_argument("--pcie", action="store_true", help="also time host-memory (PCIe-inclusive) batches")
+    p.add_argument("--wire", action="store_true",
+                   help="also time the same records sealed as one wire stream (ATLS_MODE_WIRE)")
     p.add_argument("--no-scatter", action="store_true", help="N > 1: skip the RCCL scatter/gather timing")
     return p.parse_args()
 
@@ -139,6 +145,18 @@ def main():
     alg_bytes = 2 * payload + 16 * n
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
+    # measured on-device copy bandwidth: read + write of this batch's payload buffer
+    d_cp = torch.empty_like(d_in)
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    d_cp.copy_(d_in)
+    c0.record()
+    for _ in range(10):
+        d_cp.copy_(d_in)
+    c1.record()
+    torch.cuda.synchronize(dev)
+    copy_gbps = 2 * d_in.numel() * 10 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+    del d_cp
+
     result = None
     if rank == 0:
         traffic = None
@@ -167,7 +185,8 @@ def main():
                        "parallelism": f"records sharded per GPU, dp{world}, no data-path collective"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                         "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes},
+                         "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes,
+                         "copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(achieved / copy_gbps, 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
             sample = min(n, 4096)
@@ -186,6 +205,19 @@ def main():
             for _ in range(3):
                 eng.seal_batch(recs, h_in, np.zeros(16, np.uint8), h_out, h_tags)
             result["pcie_inclusive_GiBps"] = round(3 * payload / (time.perf_counter() - t0) / 2**30, 3)
+    if args.wire and world == 1 and rank == 0:
+        # record framing on the device: header || ct || tag back to back
+        wb = workload.wire_batch(batch)
+        d_wout = torch.empty(wb["out_bytes"] + 16, dtype=torch.uint8, device=dev)
+        d_wrecs = torch.from_numpy(wb["recs"].view(np.uint8).copy()).to(dev)
+        w0, w1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for i in range(args.warmup + args.steps):
+            if i == args.warmup:
+                w0.record(stream)
+            eng.seal_batch(d_wrecs.data_ptr(), d_in, d_aux, d_wout, None, flags=flags, n=n)
+        w1.record(stream)
+        sync()
+        result["wire_GiBps"] = round(payload * args.steps / (w0.elapsed_time(w1) * 1e-3) / 2**30, 3)
     if world > 1 and not args.no_scatter:
         # host-arrival exchange beside the sealing path: rank 0 scatters / gathers a
         # 64 MiB shard per rank over RCCL; reported, not part of `value`

@@ -59,8 +59,20 @@ enum {
   ATLS_MODE_TLS = 0, /* seal: in = content (len B); AEAD input = content||content_type (len+1 B);
                         open: in = ciphertext (len B); AAD = [0x17,3,3,(len+16)>>8,(len+16)] for
                         both; nonce = static_iv ^ be64(seq). Open scans for the content type. */
-  ATLS_MODE_RAW = 1  /* AEAD over len bytes; nonce (iv_len B) then AAD (aad_len B) read from
+  ATLS_MODE_RAW = 1, /* AEAD over len bytes; nonce (iv_len B) then AAD (aad_len B) read from
                         aux + aux_off; no framing. */
+  ATLS_MODE_WIRE = 2 /* TLS mode with the record framing done on the device.
+                        seal (RecordPayloadProtection::encrypt, record.rs:162-198): in = content
+                        (len B); out + out_off receives the whole wire record, header || ct || tag
+                        (5 + len + 1 + 16 B), header = [0x17,3,3,(len+17)>>8,(len+17)].
+                        open (Record::from_raw + decrypt, record.rs:81-102, :201-240): in + in_off
+                        is a wire record (5 + len + 16 B, len = ciphertext bytes); the received
+                        header is the AAD verbatim and the tag is read from the record. A header
+                        whose type is not a RecordType (record.rs:22-33) or whose length is not
+                        len + 16 gives ATLS_DECODE_ERROR. out + out_off receives len B of inner
+                        plaintext, scanned for the content type as in TLS mode.
+                        The tags array is written on seal (a copy of the inline tag) and not read
+                        on open; it may be NULL when every record of the batch is WIRE. */
 };
 
 /* Batch flags. */

@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "build", "libatls_oracle.so")
 _lib = None
 
 SHA256, SHA384 = 32, 48
-MODE_TLS, MODE_RAW = 0, 1
+MODE_TLS, MODE_RAW, MODE_WIRE = 0, 1, 2
 
 
 class OraKey(ctypes.Structure):

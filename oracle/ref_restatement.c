@@ -815,11 +815,19 @@ int ora_record_open(uint16_t suite, const uint8_t* key, size_t key_len, const ui
 }
 
 /* ------------------------------------------------------------ batches ---- */
-enum { MODE_TLS = 0, MODE_RAW = 1 };
+enum { MODE_TLS = 0, MODE_RAW = 1, MODE_WIRE = 2 };
 
 static int seal_one(const ora_key* keys, const ora_rec* r, const uint8_t* in, const uint8_t* aux,
                     uint8_t* out, uint8_t* tag) {
   const ora_key* k = &keys[r->key_slot];
+  if (r->mode == MODE_WIRE) { /* record.rs:162-198: header || ct || tag at out_off */
+    size_t wl = 0;
+    uint8_t* w = out + r->out_off;
+    int rc = ora_record_seal(k->suite, k->key, k->key_len, k->static_iv, r->seq, r->content_type, in + r->in_off,
+                             r->len, w, &wl);
+    if (!rc && tag) memcpy(tag, w + wl - 16, 16);
+    return rc;
+  }
   if (r->mode == MODE_TLS) {
     size_t n = (size_t)r->len + 1, L = n + 16;
     uint8_t hdr[5] = {23, 3, 3, (uint8_t)(L >> 8), (uint8_t)L};
@@ -841,13 +849,24 @@ static int open_one(const ora_key* keys, const ora_rec* r, const uint8_t* in, co
                     const uint8_t* tag, uint8_t* out, ora_open_result* res) {
   const ora_key* k = &keys[r->key_slot];
   memset(res, 0, sizeof *res);
-  if (r->mode == MODE_TLS) {
+  if (r->mode == MODE_TLS || r->mode == MODE_WIRE) {
     size_t n = r->len, L = n + 16;
     uint8_t hdr[5] = {23, 3, 3, (uint8_t)(L >> 8), (uint8_t)L};
+    const uint8_t* ct = in + r->in_off;
+    if (r->mode == MODE_WIRE) { /* record.rs:81-102 from_raw, :201-220: received header = AAD */
+      const uint8_t* w = in + r->in_off;
+      if (!valid_record_type(w[0]) || (((size_t)w[3] << 8) | w[4]) != L) {
+        res->status = ORA_DECODE_ERROR;
+        return 0;
+      }
+      memcpy(hdr, w, 5);
+      ct = w + 5;
+      tag = ct + n;
+    }
     uint8_t nonce[12];
     ora_per_record_nonce(k->static_iv, r->seq, nonce);
     uint8_t* pt = out + r->out_off;
-    int rc = ora_cipher_decrypt(k->suite, k->key, k->key_len, nonce, 12, in + r->in_off, n, hdr, 5, tag, 16, pt);
+    int rc = ora_cipher_decrypt(k->suite, k->key, k->key_len, nonce, 12, ct, n, hdr, 5, tag, 16, pt);
     if (rc) {
       res->status = (rc == ORA_BAD_RECORD_MAC) ? ORA_DECRYPT_ERROR : (uint8_t)rc;
       return 0;
@@ -882,8 +901,9 @@ typedef struct {
 static void* run_job(void* p) {
   job_t* j = (job_t*)p;
   for (uint32_t i = j->lo; i < j->hi; i++) {
-    int rc = j->open ? open_one(j->keys, &j->recs[i], j->in, j->aux, j->itags + 16 * (size_t)i, j->out, &j->res[i])
-                     : seal_one(j->keys, &j->recs[i], j->in, j->aux, j->out, j->tags + 16 * (size_t)i);
+    int rc = j->open ? open_one(j->keys, &j->recs[i], j->in, j->aux, j->itags ? j->itags + 16 * (size_t)i : NULL, j->out, &j->res[i])
+                     : seal_one(j->keys, &j->recs[i], j->in, j->aux, j->out,
+                                j->tags ? j->tags + 16 * (size_t)i : NULL);
     if (rc && !j->rc) j->rc = rc;
   }
   return NULL;

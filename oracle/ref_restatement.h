@@ -115,7 +115,7 @@ typedef struct {
   uint32_t key_slot;
   uint16_t aad_len;
   uint8_t content_type;
-  uint8_t mode;
+  uint8_t mode; /* 0 TLS, 1 RAW, 2 WIRE (TLS with header || ct || tag framed in the buffer) */
   uint8_t iv_len;
   uint8_t reserved[3];
 } ora_rec;
