@@ -87,3 +87,5 @@ def test_c1_loopback_gpu():
                                             dtype=np.uint8).tobytes()
     dt, pt = c1_loopback.run_gpu(body, 2)
     assert pt == body and dt > 0
+    dt, pt = c1_loopback.run_gpu(body, 1, conns=4)  # four connections sharing each batch
+    assert pt == body and dt > 0

@@ -5,12 +5,14 @@ Keys: RFC 8448 §3 server handshake traffic secret -> write key / iv (Key::from_
 net/key_schedule.rs:40-50), sequence numbers 0..63.
 
 Two implementations of the same loop, each checked end to end (body and content types):
-  * gpu  — atls_derive_keys + one atls_seal_batch / atls_open_batch per body (anothertls_amd),
-           framing with anothertls_amd.record (net/record.rs:81-114);
+  * gpu  — atls_derive_keys, then anothertls_amd.stream.StreamBatch on each side: the writes of
+           a body (of every connection, with --conns N) sealed in one WIRE-mode atls_seal_batch
+           (the device writes header || ct || tag), the received records opened in one
+           atls_open_batch (net/stream.rs:97-150 batched);
   * cpu  — the reference's per-record path as the oracle restates it (oracle/ref_restatement.c
            ora_record_seal / ora_record_open, one record per call like tls_write / tls_read).
 Prints one JSON line: MB/s of body through seal -> socket -> open for each.
-python tools/c1_loopback.py [--reps N] [--cpu-only]"""
+python tools/c1_loopback.py [--reps N] [--cpu-only] [--conns N]"""
 import argparse
 import json
 import os
@@ -102,49 +104,65 @@ def run_cpu(body, reps):
     return _loop(seal_body, open_wire, wire_len, reps)
 
 
-def run_gpu(body, reps):
+def _tcp_pairs(n):
+    return [_pair() for _ in range(n)]
+
+
+def run_gpu(body, reps, conns=1):
+    """conns connections over 127.0.0.1, each sending `body` per rep through one StreamBatch per
+    side (anothertls_amd/stream.py): the server's writes of all connections are sealed in one
+    WIRE-mode batch, the client opens all connections' records in one batch."""
     import anothertls_amd as atls
-    from anothertls_amd import record
+    from anothertls_amd import stream
 
-    eng = atls.Engine(0)
-    keys = eng.derive_keys(0x1301, SECRET)  # one connection: the server's write key
-    eng.set_keys(keys)
-    recs = np.zeros(N_REC, atls.REC_DTYPE)
-    recs["in_off"] = np.arange(N_REC) * CONTENT
-    recs["out_off"] = np.arange(N_REC) * (CONTENT + 16)  # round16(content + type)
-    recs["len"] = CONTENT
-    recs["seq"] = np.arange(N_REC)
-    recs["content_type"] = 23
-    recs["mode"] = atls.MODE_TLS
-    inbuf = np.frombuffer(body, np.uint8)
-    out = np.zeros(N_REC * (CONTENT + 16), np.uint8)
-    tags = np.zeros(16 * N_REC, np.uint8)
-    aux = np.zeros(16, np.uint8)
+    eng_s, eng_c = atls.Engine(0), atls.Engine(0)
+    key = eng_s.derive_keys(0x1301, SECRET)[0]  # RFC 8448 server write key (Key::from_hkdf)
+    wkey = (0x1301, bytes(key["key"][:16]), bytes(key["static_iv"]))
+    pairs = _tcp_pairs(conns)
+    srv, cli = stream.StreamBatch(eng_s), stream.StreamBatch(eng_c)
+    sc = [srv.add_connection(a, wkey, wkey) for a, _ in pairs]
+    cc = [cli.add_connection(b, wkey, wkey) for _, b in pairs]
     wire_len = N_REC * (5 + CONTENT + 1 + 16)
+    frags = [body[i * CONTENT:(i + 1) * CONTENT] for i in range(N_REC)]
 
-    def seal_body():
-        eng.seal_batch(recs, inbuf, aux, out, tags)
-        return record.frame_sealed(recs, out, tags).tobytes()
+    def serve(n):
+        for _ in range(n):
+            for c in sc:
+                for f in frags:  # one tls_write per 16 KiB record, as server_https writes
+                    srv.tls_write(c, f)
+            srv.flush()
 
-    def open_wire(wire):
-        w = np.frombuffer(wire, np.uint8)
-        offs, lens = record.parse_stream(w)
-        orecs = np.zeros(len(offs), atls.REC_DTYPE)
-        orecs["in_off"] = offs + 5
-        orecs["out_off"] = offs + 5
-        orecs["len"] = lens - 16
-        orecs["seq"] = np.arange(len(offs))
-        orecs["mode"] = atls.MODE_TLS
-        itags = np.concatenate([w[o + 5 + n - 16:o + 5 + n] for o, n in zip(offs, lens)])
-        pt = np.zeros_like(w)
-        res = np.zeros(len(offs), atls.OPEN_RESULT_DTYPE)
-        eng.open_batch(orecs, w, aux, itags, pt, res)
-        assert (res["status"] == 0).all() and (res["content_type"] == 23).all(), res
-        return b"".join(pt[o + 5:o + 5 + int(c)].tobytes() for o, c in zip(offs, res["content_len"]))
+    def client(n):
+        got = None
+        for _ in range(n):
+            for c in cc:  # receive every connection's records, then open them all in one batch
+                have = 0
+                while have < wire_len:
+                    data = c.sock.recv(min(1 << 20, wire_len - have))
+                    if not data:
+                        raise ConnectionError("peer closed")
+                    cli.feed(c, data)
+                    have += len(data)
+            cli.open_pending()
+            for c in cc:
+                got = b"".join(cli.tls_read(c) for _ in range(N_REC))
+        return got
 
-    _loop(seal_body, open_wire, wire_len, 1)  # warm-up (device buffers, code objects)
-    dt, pt = _loop(seal_body, open_wire, wire_len, reps)
-    eng.close()
+    def run(n):
+        th = threading.Thread(target=serve, args=(n,))
+        t0 = time.perf_counter()
+        th.start()
+        pt = client(n)
+        th.join()
+        return time.perf_counter() - t0, pt
+
+    run(1)  # warm-up (device buffers, code objects, pinned staging)
+    dt, pt = run(reps)
+    for a, b in pairs:
+        a.close()
+        b.close()
+    eng_s.close()
+    eng_c.close()
     return dt, pt
 
 
@@ -153,6 +171,7 @@ def main():
     p.add_argument("--reps", type=int, default=8)
     p.add_argument("--cpu-reps", type=int, default=1)
     p.add_argument("--cpu-only", action="store_true")
+    p.add_argument("--conns", type=int, default=1, help="GPU path: connections sharing one batch")
     args = p.parse_args()
     body = np.random.default_rng(0xC1).integers(0, 256, N_REC * CONTENT, dtype=np.uint8).tobytes()
     res = {"config": "c1_server_https_loopback_1MiB", "records": N_REC, "suite": "TLS_AES_128_GCM_SHA256",
@@ -161,9 +180,10 @@ def main():
     assert pt == body
     res["cpu_reference_MBps"] = round(args.cpu_reps * len(body) / dt / 1e6, 3)
     if not args.cpu_only:
-        dt, pt = run_gpu(body, args.reps)
+        dt, pt = run_gpu(body, args.reps, args.conns)
         assert pt == body
-        res["gpu_MBps"] = round(args.reps * len(body) / dt / 1e6, 1)
+        res["gpu_conns"] = args.conns
+        res["gpu_MBps"] = round(args.reps * args.conns * len(body) / dt / 1e6, 1)
     print(json.dumps(res), flush=True)
 
 
