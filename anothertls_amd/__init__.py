@@ -57,6 +57,9 @@ _lib.atls_seal_batch.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_voi
 _lib.atls_open_batch.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
                                  _c.c_void_p, _c.c_void_p, _c.c_uint32]
 _lib.atls_derive_keys.argtypes = [_c.c_void_p, _c.c_uint16, _c.c_void_p, _c.c_size_t, _c.c_uint32, _c.c_void_p]
+_lib.atls_aes_blocks.argtypes = [_c.c_void_p, _c.c_int, _c.c_uint32, _c.c_void_p, _c.c_void_p, _c.c_size_t,
+                                 _c.c_uint32]
+_lib.atls_aes_block.argtypes = [_c.c_int, _c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_void_p]
 _lib.atls_device_arch.restype = _c.c_char_p
 
 
@@ -179,6 +182,37 @@ class Poly1305(_DeviceCipher):
     _suite = CipherSuite.TLS_CHACHA20_POLY1305_SHA256
 
 
+class AES:
+    """crypto/aes/cipher.rs:159-215 ``AES``: ``AES.init(key, blocksize)`` then ``encrypt`` /
+    ``decrypt`` of one 16-byte block, on the device (atls_aes_block). ``blocksize`` is the key
+    size in bits (cipher.rs:141-156 Blocksize); a key of another length is ILLEGAL_PARAMETER
+    where the reference would index out of bounds."""
+
+    def __init__(self, key, blocksize=None):
+        self.key = bytes(key)
+        bits = len(self.key) * 8 if blocksize is None else int(blocksize)
+        if bits not in (128, 192, 256) or bits != len(self.key) * 8:
+            raise TlsError(TlsError.ILLEGAL_PARAMETER)
+
+    @classmethod
+    def init(cls, key, blocksize=None):
+        return cls(key, blocksize)
+
+    def _run(self, decrypt, block):
+        block = bytes(block)
+        if len(block) != 16:
+            raise TlsError(TlsError.ILLEGAL_PARAMETER)
+        out = _c.create_string_buffer(16)
+        _check(_lib.atls_aes_block(int(decrypt), self.key, len(self.key), block, out))
+        return out.raw
+
+    def encrypt(self, block):  # cipher.rs:175-194
+        return self._run(False, block)
+
+    def decrypt(self, block):  # cipher.rs:196-215
+        return self._run(True, block)
+
+
 def device_available():
     """True when the HIP runtime sees a device the engine can open."""
     e = _lib.atls_engine_create(int(os.environ.get("ATLS_DEVICE", "0")))
@@ -257,6 +291,11 @@ class Engine:
     def seal_batch(self, recs, inp, aux, out, tags, flags=0, n=None):
         n = len(recs) if n is None else n
         _check(_lib.atls_seal_batch(self._e, _ptr(recs), n, _ptr(inp), _ptr(aux), _ptr(out), _ptr(tags), flags))
+
+    def aes_blocks(self, decrypt, key_slot, inp, out, flags=0, nblocks=None):
+        """AES::encrypt / decrypt of every 16-byte block of inp under key slot key_slot."""
+        nb = (inp.nbytes if hasattr(inp, "nbytes") else inp.numel()) // 16 if nblocks is None else nblocks
+        _check(_lib.atls_aes_blocks(self._e, int(decrypt), int(key_slot), _ptr(inp), _ptr(out), nb, flags))
 
     def open_batch(self, recs, inp, aux, tags, out, results, flags=0, n=None):
         n = len(recs) if n is None else n

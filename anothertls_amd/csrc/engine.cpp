@@ -23,6 +23,8 @@
 #include "plan.h"
 
 extern "C" int atls_launch_build_t0(uint32_t* t0, hipStream_t s);
+extern "C" int atls_launch_aes_blocks(int decrypt, const void* ks, const uint8_t* in, uint8_t* out, uint64_t nblocks,
+                                      uint32_t* err, int grid, hipStream_t s);
 extern "C" int atls_launch_key_setup(const atls_key* keys, uint32_t n, void* ks, hipStream_t s);
 extern "C" int atls_launch_plan(int open, const void* ks, const atls_rec* recs, uint32_t n, uint32_t n_slots,
                                 atls_open_result* res, uint32_t* err, void* P, uint8_t* keys, uint32_t* idx,
@@ -330,6 +332,12 @@ atls_engine* default_engine() {
   return g_default;
 }
 
+// Serialises the single-call entry points, which share the default engine's key slot 0.
+std::mutex& single_mu() {
+  static std::mutex m;
+  return m;
+}
+
 // One Cipher::encrypt / decrypt call as a single RAW record.
 int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
            const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, const uint8_t* tag_in, size_t tag_len,
@@ -353,8 +361,7 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
   k.iv_len = 12;
   std::memcpy(k.key, key, key_len);
   // One engine, one slot: serialise single calls (the batch API is the throughput path).
-  static std::mutex single_mu;
-  std::lock_guard<std::mutex> lk(single_mu);
+  std::lock_guard<std::mutex> lk(single_mu());
   int rc = atls_set_keys(e, &k, 1);
   if (rc) return rc;
   std::vector<uint8_t> aux(iv_len + aad_len + 1);
@@ -518,6 +525,52 @@ int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, siz
   if (hipMemcpyAsync(out_keys, e->dkeys.p, sizeof(atls_key) * (size_t)n, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
     return ATLS_INTERNAL_ERROR;
   return hipStreamSynchronize(e->stream) == hipSuccess ? ATLS_OK : ATLS_INTERNAL_ERROR;
+}
+
+int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* in, void* out, size_t nblocks,
+                    uint32_t flags) {
+  if (!e) return ATLS_INTERNAL_ERROR;
+  if (nblocks == 0) return ATLS_OK;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  if (key_slot >= e->n_slots) return ATLS_ILLEGAL_PARAMETER;
+  hipStream_t s = e->stream;
+  const size_t bytes = 16 * nblocks;
+  const bool dev = flags & ATLS_FLAG_DEVICE_PTRS;
+  const uint8_t* d_in = (const uint8_t*)in;
+  uint8_t* d_out = (uint8_t*)out;
+  if (!dev) {
+    if (!e->in.reserve(bytes) || !e->out.reserve(bytes) ||
+        hipMemcpyAsync(e->in.p, in, bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    d_in = (const uint8_t*)e->in.p;
+    d_out = (uint8_t*)e->out.p;
+  }
+  if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess ||
+      atls_launch_aes_blocks(decrypt, (const atls::KeySched*)e->ks.p + key_slot, d_in, d_out, nblocks,
+                             (uint32_t*)e->err.p, e->cus * 8, s))
+    return ATLS_INTERNAL_ERROR;
+  if (!dev) {
+    if (hipMemcpyAsync(out, e->out.p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+    return finish(e, flags & ~ATLS_FLAG_NO_SYNC);
+  }
+  return finish(e, flags);
+}
+
+int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_t in[16], uint8_t out[16]) {
+  if (key_len != 16 && key_len != 24 && key_len != 32) return ATLS_ILLEGAL_PARAMETER;  // AES::init key sizes
+  atls_engine* e = default_engine();
+  if (!e) return ATLS_INTERNAL_ERROR;
+  atls_key k;
+  std::memset(&k, 0, sizeof k);
+  k.suite = ATLS_TLS_AES_128_GCM_SHA256;  // any AES suite: the slot only carries the key
+  k.key_len = (uint8_t)key_len;
+  k.iv_len = 12;
+  std::memcpy(k.key, key, key_len);
+  std::lock_guard<std::mutex> lk(single_mu());
+  int rc = atls_set_keys(e, &k, 1);
+  if (rc) return rc;
+  return atls_aes_blocks(e, decrypt, 0, in, out, 1, 0);
 }
 
 }  // extern "C"

@@ -156,6 +156,16 @@ int atls_open_batch(atls_engine* e, const atls_rec* recs, uint32_t n, const void
 int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, size_t secret_len, uint32_t n,
                      atls_key* out_keys);
 
+/* The AES block cipher, AES::init + AES::encrypt / AES::decrypt (crypto/aes/cipher.rs:167-215),
+ * over nblocks independent 16-byte blocks (ECB) under key slot key_slot of the engine's table
+ * (an AES suite slot; otherwise ATLS_ILLEGAL_PARAMETER). Not on the record path -- GCM only
+ * encrypts -- but the reference's AES API, on the device. flags: ATLS_FLAG_DEVICE_PTRS and
+ * ATLS_FLAG_NO_SYNC as for the batches. */
+int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* in, void* out, size_t nblocks,
+                    uint32_t flags);
+/* One block with a raw key (16/24/32 B) on the process-default engine. */
+int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_t in[16], uint8_t out[16]);
+
 /* Library info: ABI version and the device arch the code objects were built for ("gfx950"). */
 int atls_abi_version(void);
 const char* atls_device_arch(void);

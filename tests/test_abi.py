@@ -80,6 +80,9 @@ def test_parameter_errors_before_device():
     with pytest.raises(atls.TlsError) as e:
         atls.Gcm().decrypt(b"k" * 16, b"i" * 12, b"x", b"", b"short")
     assert e.value.code == 20
+    with pytest.raises(atls.TlsError) as e:  # AES::init with a key that is not the block size
+        atls.AES.init(b"k" * 16, 256)
+    assert e.value.code == 47
 
 
 @pytest.mark.skipif(atls.device_available(), reason="a GPU is present")
@@ -89,4 +92,7 @@ def test_no_gpu_fails_loudly():
     assert e.value.code == 80
     with pytest.raises(atls.TlsError) as e:
         atls.Engine(0)
+    assert e.value.code == 80
+    with pytest.raises(atls.TlsError) as e:
+        atls.AES.init(b"k" * 16).encrypt(bytes(16))
     assert e.value.code == 80
