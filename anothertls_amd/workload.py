@@ -86,10 +86,13 @@ def wire_open_descs(sealed):
     return recs, int(_round16(L).sum()) if len(recs) else 0
 
 
-def config_batch(name, n=None, first=0):
-    """Descriptors for a BASELINE config: records first .. first+n-1 of it (default: all)."""
+def config_batch(name, n=None, first=0, n_keys=None):
+    """Descriptors for a BASELINE config: records first .. first+n-1 of it (default: all).
+    n_keys overrides the config's 4,096 connections (n_keys = records: a key per record, the
+    SURVEY §8d worst case)."""
     suite, n_full, lens = CONFIGS[name]
     n = n_full - first if n is None else n
+    nk = min(4096, n_full) if n_keys is None else int(n_keys)
     if suite == "mixed":
         rng = np.random.default_rng(SEEDS["layout"])
         lo, hi = lens
@@ -100,8 +103,8 @@ def config_batch(name, n=None, first=0):
             return np.where(r.random(k) < 0.5, int(CipherSuite.TLS_AES_128_GCM_SHA256),
                             int(CipherSuite.TLS_CHACHA20_POLY1305_SHA256)).astype(np.uint16)
 
-        return tls_batch(n, L, suites, n_keys=min(4096, n_full), first=first, shrink_keys=False)
-    return tls_batch(n, lens, int(suite), n_keys=min(4096, n_full), first=first, shrink_keys=False)
+        return tls_batch(n, L, suites, n_keys=nk, first=first, shrink_keys=False)
+    return tls_batch(n, lens, int(suite), n_keys=nk, first=first, shrink_keys=False)
 
 
 # Configs BASELINE.json quotes on 8 GPUs: their records are split evenly over 8 ranks, and a rank
@@ -114,8 +117,8 @@ def records_per_rank(name):
     return n_full // 8 if name in EIGHT_GPU_CONFIGS else n_full
 
 
-def shard_batch(name, rank, n=None):
+def shard_batch(name, rank, n=None, n_keys=None):
     """Rank `rank`'s shard: records rank*n .. rank*n+n-1 of the config's record stream (key slots,
     sequence numbers and lengths as in the unsharded batch). n defaults to records_per_rank()."""
     n = records_per_rank(name) if n is None else n
-    return config_batch(name, n=n, first=rank * n)
+    return config_batch(name, n=n, first=rank * n, n_keys=n_keys)

@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c2_aes128gcm_64Ki_x_16KiB")
     p.add_argument("--records", type=int, default=None, help="override records per GPU")
+    p.add_argument("--key-slots", type=int, default=None,
+                   help="override the config's 4096 connections (= records: one key per record)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=16,
@@ -103,7 +105,7 @@ def main():
     from anothertls_amd import workload
 
     # this rank's shard of the config's record stream (weak scaling: fixed records per GPU)
-    batch = workload.shard_batch(args.config, rank, n=args.records)
+    batch = workload.shard_batch(args.config, rank, n=args.records, n_keys=args.key_slots)
     recs = batch["recs"]
     n = len(recs)
     eng = atls.Engine(local)
