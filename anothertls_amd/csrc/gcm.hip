@@ -29,7 +29,8 @@ namespace atls {
 #define ATLS_GHASH_W 0  // > 0: GHASH lookups issued per LDS round trip (ghash_mul_tab_wide); 0: compiler schedule
 #endif
 #ifndef ATLS_DBG_SKIP
-#define ATLS_DBG_SKIP 0  // timing experiments only (wrong results): 1 lane combine, 2 general steps, 4 GHASH table
+#define ATLS_DBG_SKIP 0  // timing experiments only (wrong results): 1 lane combine, 2 general steps, 4 GHASH
+                         // table, 8 GHASH multiply in general steps, 16 last step, 32 first step
 #endif
 #ifndef ATLS_CTR_CACHE
 #define ATLS_CTR_CACHE 1
@@ -330,6 +331,8 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       continue;
     }
     if (ATLS_DBG_SKIP & 2) continue;
+    if ((ATLS_DBG_SKIP & 16) && base + 64u >= S) continue;
+    if ((ATLS_DBG_SKIP & 32) && base == 0u) continue;
     // counter block J0 + c (gcm.rs:89-96): c = s - na for data block s - 1 - na, 0 for slots 0..na
     const uint32_t c = (s > na) ? (s - na) : 0u;
     uint32_t cb[4] = {j0[0], j0[1], j0[2], j0[3]};
@@ -419,7 +422,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     }
     // Y <- Y * H^64 ^ B on the lanes that hold a GHASH block; the others keep Y (s_last below).
     uint32_t yn[4] = {y[0], y[1], y[2], y[3]};
-    ghash_mul<ATLS_GHASH_W>(yn, wb);
+    if (!(ATLS_DBG_SKIP & 8)) ghash_mul<ATLS_GHASH_W>(yn, wb);
     if (s >= 1 && s <= m) {
 #pragma unroll
       for (int w = 0; w < 4; w++) y[w] = yn[w] ^ B[w];
