@@ -1,5 +1,6 @@
-// Bitsliced AES for gfx950: 32 blocks per lane, AES rounds as v_bitop3_b32 / v_perm_b32 /
-// v_alignbit_b32 logic on the VALU (no table lookups).
+// Bitsliced AES for gfx950: 8 G blocks per lane, AES rounds as v_bitop3_b32 / v_perm_b32 /
+// v_alignbit_b32 logic on the VALU (no table lookups). Used by the keystream kernel
+// (ks_bs.hip), which runs on the VALU beside the LDS-bound T-table kernel (gcm.hip).
 //
 // Row-plane layout: st[g][r][j], g = block group (blocks 8g..8g+7), r = state row, j = bit
 // significance 7 - j (j = 0 is the MSB, the S-box circuit's U0). Bit 8c + b of a word is bit
@@ -30,7 +31,9 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 __device__ __forceinline__ uint32_t bmask(uint32_t w, int b) { return (uint32_t)((int32_t)(w << (31 - b)) >> 31); }
 __device__ __forceinline__ uint32_t rotr(uint32_t w, int n) { return n ? __builtin_amdgcn_alignbit(w, w, n) : w; }
 
-typedef uint32_t State[4][4][8];  // [group][row][significance 7 - j]
+template <int G>
+using StateG = uint32_t[G][4][8];  // [group][row][significance 7 - j]
+typedef StateG<4> State;
 typedef uint32_t Masks[4][8];     // [row][significance 7 - j]
 
 // Round-key masks from the four raw key words (or any four column words, e.g. a nonce XOR key).
@@ -52,16 +55,18 @@ __device__ __forceinline__ void make_masks(const uint32_t (&w)[4], Masks& m) {
     }
 }
 
-__device__ __forceinline__ void sub_bytes(State& st) {
+template <int G>
+__device__ __forceinline__ void sub_bytes(StateG<G>& st) {
 #pragma unroll
-  for (int g = 0; g < 4; g++)
+  for (int g = 0; g < G; g++)
 #pragma unroll
     for (int r = 0; r < 4; r++) sbox_bs(st[g][r]);
 }
 
-__device__ __forceinline__ void add_round_key(State& st, const Masks& m) {
+template <int G>
+__device__ __forceinline__ void add_round_key(StateG<G>& st, const Masks& m) {
 #pragma unroll
-  for (int g = 0; g < 4; g++)
+  for (int g = 0; g < G; g++)
 #pragma unroll
     for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -73,9 +78,10 @@ __device__ __forceinline__ void add_round_key(State& st, const Masks& m) {
 // u = a_r ^ a_{r+1} at bit t and folds u's bit 7 into bits 0, 1, 3, 4 (0x1b). Significances are
 // rewritten in place from 7 down to 0, so each step reads only not-yet-written lower bits; u's
 // bit 7 is saved first. Temporaries: 4 + 4 words per group.
-__device__ __forceinline__ void shift_mix_ark(State& st, const Masks& m) {
+template <int G>
+__device__ __forceinline__ void shift_mix_ark(StateG<G>& st, const Masks& m) {
 #pragma unroll
-  for (int g = 0; g < 4; g++) {
+  for (int g = 0; g < G; g++) {
     uint32_t (&a)[4][8] = st[g];  // a[r][7 - t]
 #pragma unroll
     for (int r = 1; r < 4; r++)
@@ -106,9 +112,10 @@ __device__ __forceinline__ void shift_mix_ark(State& st, const Masks& m) {
 }
 
 // Final round: ShiftRows + AddRoundKey (no MixColumns).
-__device__ __forceinline__ void shift_ark(State& st, const Masks& m) {
+template <int G>
+__device__ __forceinline__ void shift_ark(StateG<G>& st, const Masks& m) {
 #pragma unroll
-  for (int g = 0; g < 4; g++)
+  for (int g = 0; g < G; g++)
 #pragma unroll
     for (int r = 0; r < 4; r++)
 #pragma unroll

@@ -173,7 +173,7 @@ __device__ unsigned long long g_tt_stamps[8];
 #define TT_STAMP(var)
 #endif
 
-template <int NR, bool OPEN>
+template <int NR, bool OPEN, bool KS>
 __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx,
                            uint32_t lb, uint32_t wb, int lane) {
   TT_STAMP(t_start);
@@ -273,7 +273,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   // Counter cache (CtrCache): every 64-slot step's counters share ctr >> 8 when the counter of slot
   // `base` is a multiple of 64 -- records with one AAD block (all TLS records) and a 96-bit IV.
   // Lane j holds the words of hi = j, enough for records below 2^14 blocks (256 KiB).
-  const bool use_cache = ATLS_CTR_CACHE && is96 && na == 1u && S <= 64u * 256u;
+  // KS launch: this record's counter blocks were encrypted by ks_bs.hip (bitsliced, on the VALU)
+  const bool use_ks = KS && A.ks_ok[rec_idx];
+  const uint8_t* kp = KS ? A.ksb + 16ull * kKsStride * rec_idx : nullptr;
+  const bool use_cache = ATLS_CTR_CACHE && is96 && na == 1u && S <= 64u * 256u && !use_ks;
   const uint32_t nraw[3] = {bswap32(j0[0]), bswap32(j0[1]), bswap32(j0[2])};
   const uint32_t lane_addr = ((uint32_t)lane << 8) | lb;  // T0 address of byte value `lane`
   const uint32_t k15 = rk[3] >> 24;                       // rk0 byte 15
@@ -306,7 +309,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       const uint4 Pu = ld16(src + off);
       const v4u32 P = {Pu.x, Pu.y, Pu.z, Pu.w};
       uint32_t st[4];
-      if (use_cache) {
+      if (use_ks) {
+        const uint4 kv = ld16(kp + 16u * (s - na));
+        st[0] = kv.x; st[1] = kv.y; st[2] = kv.z; st[3] = kv.w;
+      } else if (use_cache) {
         const uint32_t c0 = j0[3] + base - na;  // counter of lane 0, a multiple of 64
         aes_cached(st, lane_addr ^ (((c0 & 0xffu) ^ k15) << 8), c0 >> 8);
       } else {
@@ -366,7 +372,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
         }
       }
     }
-    if (use_cache) {  // ctr = 1 for slots 0..na, else 1 + s - na: the step's ctr >> 8 is lane 63's
+    if (use_ks) {  // keystream block c (c = 0: E_K(J0)); lanes past the record read in-bounds junk
+      const uint4 kv = ld16(kp + 16u * min(c, kKsStride - 1u));
+      st[0] = kv.x; st[1] = kv.y; st[2] = kv.z; st[3] = kv.w;
+    } else if (use_cache) {  // ctr = 1 for slots 0..na, else 1 + s - na: the step's ctr >> 8 is lane 63's
       const uint32_t ctr = cb[3];
       const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)ctr, 63) >> 8;
       aes_cached(st, perm((ctr & 0xffu) ^ k15, lb, 0x0c0c0400u), hi);
@@ -488,7 +497,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 // footprint (64 KiB tables + 8 KiB per wave) is what limits residency. One launch per AES round
 // count (a kernel holds only that count's round keys); the waves take the records of that round
 // count's work list (plan.hip, longest first) round-robin.
-template <bool OPEN, int kWaves, int NR>
+template <bool OPEN, int kWaves, int NR, bool KS = false>
 __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
@@ -521,7 +530,7 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
         continue;
       }
     }
-    gcm_record<NR, OPEN>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
+    gcm_record<NR, OPEN, KS>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
     wave_lds_sync();  // table reads of this record done before the next record rebuilds it
   }
 }
@@ -558,6 +567,31 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   }
   ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(12)
 #undef ATLS_LAUNCH
+#undef ATLS_LAUNCH_NR
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}
+
+// The KS launch of a hybrid batch (engine.cpp): records [0, n) of a direct batch whose keystream
+// atls_launch_ks wrote to ksb (ok per record in ks_ok; records without it use the T-tables).
+extern "C" int atls_launch_gcm_ks(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
+                                  const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
+                                  atls_open_result* res, const uint32_t* t0, const uint8_t* ksb, const uint8_t* ks_ok,
+                                  uint32_t* err, uint32_t n_slots, int nr_mask, int grid, hipStream_t s) {
+  if (n == 0) return 0;
+  atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, nullptr, nullptr,
+                  err, n_slots, ksb, ks_ok};
+  constexpr int W = 12;
+  const uint32_t want = (n + W - 1) / W;
+  const uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
+  const dim3 block(64 * W);
+  const size_t lds = atls::lds_bytes(W);
+#define ATLS_LAUNCH_NR(NR)                                                                          \
+  if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR, true>), dim3(g), block, lds, s, A);   \
+  else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR, true>), dim3(g), block, lds, s, A);
+  if (nr_mask == 1) { ATLS_LAUNCH_NR(10) }
+  else if (nr_mask == 2) { ATLS_LAUNCH_NR(12) }
+  else if (nr_mask == 4) { ATLS_LAUNCH_NR(14) }
+  else return ATLS_INTERNAL_ERROR;
 #undef ATLS_LAUNCH_NR
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }

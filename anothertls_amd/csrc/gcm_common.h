@@ -200,6 +200,8 @@ struct GcmArgs {
   PlanHdr* plan;
   uint32_t* err;           // direct mode: sticky error word
   uint32_t n_slots;        // direct mode: key-table size
+  const uint8_t* ksb;      // KS launches: keystream of ks_bs.hip, kKsStride blocks per record
+  const uint8_t* ks_ok;    // KS launches: per record, 1 = keystream present (else T-tables)
 };
 
 // Open result for one record (record.rs:203-240 decrypt + padding scan). lastnz = (position <<

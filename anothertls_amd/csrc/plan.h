@@ -8,6 +8,9 @@ constexpr uint32_t kListGcm10 = 0, kListGcm12 = 1, kListGcm14 = 2, kListChacha =
 constexpr int kPlanLists = 4;
 constexpr int kPlanClasses = 16;  // length classes min(len >> 10, 15), longest first
 constexpr uint32_t kPlanReject = 0xffu;
+// Keystream buffer of ks_bs.hip: kKsStride 16-byte blocks per record (counters 0 .. nb + 1).
+constexpr uint32_t kKsUnits = 132;           // 8-counter units per record
+constexpr uint32_t kKsStride = 8 * kKsUnits;  // AEAD <= 16,848 B
 
 struct PlanHdr {
   uint32_t off[kPlanLists + 1];                  // list l = idx[off[l] .. off[l+1])

@@ -1,8 +1,6 @@
-// Microbenchmark: bitsliced AES-128 rounds (row-plane layout, aes_bs.h) on the VALU with
-// wave-uniform round-key masks in SGPRs, G groups of 8 blocks per lane, no memory traffic.
-// Prints CU-cycles per 16-B block at the nominal 2.4 GHz for each variant.
+// Burn kernel for co-residency experiments: aes_ubench's bitsliced AES rounds (VALU only, no
+// memory traffic) callable from Python beside the engine (tools/corun_gcm.py).
 #include <hip/hip_runtime.h>
-#include <stdio.h>
 #include <stdint.h>
 #include "../../anothertls_amd/csrc/sbox_bs.h"
 
@@ -80,33 +78,11 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(G == 1
   out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
-template <int G, int WPB>
-void run(const uint32_t* dm, uint32_t* dout, int blocks_per_cu) {
-  const int grid = 256 * blocks_per_cu, iters = 64;
-  hipLaunchKernelGGL((k_bs<G, WPB>), dim3(grid), dim3(64 * WPB), 0, 0, dm, dout, 2);
-  hipEvent_t a, b;
-  hipEventCreate(&a); hipEventCreate(&b);
-  hipEventRecord(a);
-  hipLaunchKernelGGL((k_bs<G, WPB>), dim3(grid), dim3(64 * WPB), 0, 0, dm, dout, iters);
-  hipEventRecord(b);
-  hipEventSynchronize(b);
-  float ms; hipEventElapsedTime(&ms, a, b);
-  const double blocks = (double)grid * 64 * WPB * 8 * G * iters;
-  const double cyc = 256.0 * 2.4e9 * ms * 1e-3 / blocks;
-  printf("bitsliced AES-128 G=%d waves/WG=%d WG/CU-ish=%d: %.3f ms, %.2f CU-cycles/block, %.1f GB/s keystream\n", G, WPB,
-         blocks_per_cu, ms, cyc, blocks * 16 / (ms * 1e-3) / 1e9);
-}
 
-int main() {
-  uint32_t *dm, *dout;
-  hipMalloc(&dm, 4096);
-  hipMemset(dm, 0x5a, 4096);
-  hipMalloc(&dout, 256 * 64 * 1024 * 4);
-  run<1, 4>(dm, dout, 8);
-  run<2, 4>(dm, dout, 4);
-  run<2, 4>(dm, dout, 8);
-  run<2, 8>(dm, dout, 2);
-  run<4, 4>(dm, dout, 2);
-  run<4, 4>(dm, dout, 4);
-  return 0;
+extern "C" int bs_burn(void* stream, int g, int grid, int iters, const uint32_t* masks, uint32_t* out) {
+  if (g == 1)
+    hipLaunchKernelGGL((k_bs<1, 4>), dim3(grid), dim3(256), 0, (hipStream_t)stream, masks, out, iters);
+  else
+    hipLaunchKernelGGL((k_bs<2, 4>), dim3(grid), dim3(256), 0, (hipStream_t)stream, masks, out, iters);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
 }
