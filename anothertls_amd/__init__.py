@@ -288,17 +288,32 @@ class Engine:
         _check(_lib.atls_derive_keys(self._e, int(suite), buf.ctypes.data, hl, n, out.ctypes.data))
         return out
 
+    def _after_torch(self, *xs):
+        """Device tensors from PyTorch: the engine's stream waits for the work already queued on
+        torch's current stream (e.g. the fill of a fresh torch.zeros output), without a host sync."""
+        for x in xs:
+            if getattr(x, "is_cuda", False):
+                import torch
+
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(x.device))
+                torch.cuda.ExternalStream(self.stream, device=x.device).wait_event(ev)
+                return
+
     def seal_batch(self, recs, inp, aux, out, tags, flags=0, n=None):
         n = len(recs) if n is None else n
+        self._after_torch(recs, inp, aux, out, tags)
         _check(_lib.atls_seal_batch(self._e, _ptr(recs), n, _ptr(inp), _ptr(aux), _ptr(out), _ptr(tags), flags))
 
     def aes_blocks(self, decrypt, key_slot, inp, out, flags=0, nblocks=None):
         """AES::encrypt / decrypt of every 16-byte block of inp under key slot key_slot."""
+        self._after_torch(inp, out)
         nb = (inp.nbytes if hasattr(inp, "nbytes") else inp.numel()) // 16 if nblocks is None else nblocks
         _check(_lib.atls_aes_blocks(self._e, int(decrypt), int(key_slot), _ptr(inp), _ptr(out), nb, flags))
 
     def open_batch(self, recs, inp, aux, tags, out, results, flags=0, n=None):
         n = len(recs) if n is None else n
+        self._after_torch(recs, inp, aux, tags, out, results)
         _check(_lib.atls_open_batch(self._e, _ptr(recs), n, _ptr(inp), _ptr(aux), _ptr(tags), _ptr(out),
                                     _ptr(results), flags))
 

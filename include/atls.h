@@ -166,6 +166,30 @@ int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* 
 /* One block with a raw key (16/24/32 B) on the process-default engine. */
 int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_t in[16], uint8_t out[16]);
 
+/* ---- Batched record streams (TlsStream::tls_write / tls_read, net/stream.rs:32-150) -------
+ * Many connections over one engine: atls_sb_write queues a connection's records (fragmented at
+ * 2^14 bytes, RFC 8446 §5.1), atls_sb_flush seals the queued records of every connection in one
+ * ATLS_MODE_WIRE batch and send()s each connection's wire bytes; received bytes (atls_sb_recv
+ * from the socket, or atls_sb_feed) are split into whole records (Record::from_raw,
+ * record.rs:81-102), atls_sb_open_pending opens every connection's complete records in one
+ * batch, atls_sb_read returns the next application-data record of a connection (blocking:
+ * receives and opens as needed; UnexpectedMessage (10) for other content types, stream.rs:112-116;
+ * BrokenPipe (254) at end of stream). Each connection has a write key and a read key with their
+ * own sequence numbers (key_schedule.rs:51-64); a record that fails ends its connection with
+ * the record layer's error (50 / 51), which later calls return. Functions returning long give
+ * a count (>= 0) or minus a TlsError code. One batch per thread at a time. */
+typedef struct atls_stream_batch atls_stream_batch;
+atls_stream_batch* atls_sb_create(atls_engine* e);
+void atls_sb_destroy(atls_stream_batch* sb);
+/* fd: a connected stream socket; returns the connection id (>= 0) or -code. */
+int atls_sb_add_connection(atls_stream_batch* sb, int fd, const atls_key* write_key, const atls_key* read_key);
+int atls_sb_write(atls_stream_batch* sb, int conn, uint8_t content_type, const uint8_t* data, size_t len);
+long atls_sb_flush(atls_stream_batch* sb);                       /* records sealed and sent */
+int atls_sb_feed(atls_stream_batch* sb, int conn, const uint8_t* data, size_t len);
+long atls_sb_recv(atls_stream_batch* sb, int conn, size_t max_bytes); /* bytes read; 0 at EOF */
+long atls_sb_open_pending(atls_stream_batch* sb);                /* records opened */
+int atls_sb_read(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size_t* out_len);
+
 /* Library info: ABI version and the device arch the code objects were built for ("gfx950"). */
 int atls_abi_version(void);
 const char* atls_device_arch(void);

@@ -24,9 +24,12 @@ def atls():
     return a
 
 
-def _engine(atls, f):
-    old = {k: os.environ.get(k) for k in ("ATLS_HYBRID", "ATLS_HYBRID_MIN")}
+def _engine(atls, f, staged=False):
+    """An engine with the hybrid split forced on; staged: host batches go through the one-piece
+    staging path (which splits) rather than the chunk pipeline (which does not)."""
+    old = {k: os.environ.get(k) for k in ("ATLS_HYBRID", "ATLS_HYBRID_MIN", "ATLS_NO_PIPELINE")}
     os.environ["ATLS_HYBRID"], os.environ["ATLS_HYBRID_MIN"] = str(f), "1"
+    os.environ["ATLS_NO_PIPELINE"] = "1" if staged else "0"
     try:
         return atls.Engine(0)
     finally:
@@ -80,7 +83,7 @@ def test_hybrid_seal_open_vs_oracle(atls, suite, klen, device):
 
     keys, recs, aux, inbuf = _batch(atls, suite, klen, 600, klen)
     want_out, want_tags = _oracle(keys, recs, inbuf, aux)
-    eng = _engine(atls, 0.5)
+    eng = _engine(atls, 0.5, staged=not device)
     eng.set_keys(keys)
     dev = torch.device("cuda", 0)
     n = len(recs)

@@ -1,0 +1,6 @@
+#!/bin/bash
+# Host-only tools linked against anothertls_amd/libatls.so (built by __graft_entry__.build()).
+set -e
+cd "$(dirname "$0")/.."
+g++ -O2 -std=c++17 -Wall -Iinclude tools/c1_loopback_native.cpp -Lanothertls_amd -latls \
+    -Wl,-rpath,'$ORIGIN/../anothertls_amd' -lpthread -o tools/c1_loopback_native

@@ -1,0 +1,123 @@
+// BASELINE config C1 (server_https over loopback), native: a server thread sends `reps` bodies of
+// 1 MiB (64 records of 16 KiB, TLS_AES_128_GCM_SHA256) on each of `conns` TCP connections over
+// 127.0.0.1 through one atls_stream_batch (every body's records of every connection sealed in
+// one WIRE-mode batch); the client receives through another batch, which opens every
+// connection's pending records together, and checks every byte. Keys: the RFC 8448 §3 server
+// handshake traffic secret through atls_derive_keys (Key::from_hkdf, key_schedule.rs:40-50).
+// Prints one JSON line: MB/s of body through seal -> socket -> open.
+//
+// Built by __graft_entry__.build() with tools/build_native.sh (g++, linked to libatls.so).
+// Usage: tools/c1_loopback_native [reps=8] [conns=1]
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "atls.h"
+
+namespace {
+
+constexpr int kRecords = 64;
+constexpr size_t kContent = 16384;
+constexpr size_t kBody = kRecords * kContent;
+
+bool tcp_pair(int* server_fd, int* client_fd) {
+  const int ls = socket(AF_INET, SOCK_STREAM, 0);
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  socklen_t al = sizeof a;
+  if (ls < 0 || bind(ls, (sockaddr*)&a, sizeof a) || listen(ls, 1) || getsockname(ls, (sockaddr*)&a, &al)) return false;
+  const int c = socket(AF_INET, SOCK_STREAM, 0);
+  if (c < 0 || connect(c, (sockaddr*)&a, sizeof a)) return false;
+  const int s = accept(ls, nullptr, nullptr);
+  close(ls);
+  if (s < 0) return false;
+  const int buf = 4 << 20;
+  for (int fd : {s, c}) {
+    setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &buf, sizeof buf);
+    setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
+  }
+  *server_fd = s;
+  *client_fd = c;
+  return true;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? std::atoi(argv[1]) : 8;
+  const int conns = argc > 2 ? std::atoi(argv[2]) : 1;
+  atls_engine* es = atls_engine_create(0);
+  atls_engine* ec = atls_engine_create(0);
+  if (!es || !ec) {
+    std::fprintf(stderr, "c1_loopback_native: no usable HIP device\n");
+    return 2;
+  }
+  static const uint8_t kSecret[32] = {0xb6, 0x7b, 0x7d, 0x69, 0x0c, 0xc1, 0x6c, 0x4e, 0x75, 0xe5, 0x42,
+                                      0x13, 0xcb, 0x2d, 0x37, 0xb4, 0xe9, 0xc9, 0x12, 0xbc, 0xde, 0xd9,
+                                      0x10, 0x5d, 0x42, 0xbe, 0xfd, 0x59, 0xd3, 0x91, 0xad, 0x38};
+  atls_key key;
+  if (atls_derive_keys(es, ATLS_TLS_AES_128_GCM_SHA256, kSecret, 32, 1, &key)) return 3;
+  std::vector<uint8_t> body(kBody);
+  uint64_t x = 0xC1;
+  for (auto& b : body) {
+    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+    b = (uint8_t)x;
+  }
+  atls_stream_batch* ss = atls_sb_create(es);
+  atls_stream_batch* cs = atls_sb_create(ec);
+  std::vector<int> sc(conns), cc(conns), fds;
+  for (int i = 0; i < conns; i++) {
+    int s, c;
+    if (!tcp_pair(&s, &c)) return 4;
+    fds.push_back(s);
+    fds.push_back(c);
+    sc[i] = atls_sb_add_connection(ss, s, &key, &key);
+    cc[i] = atls_sb_add_connection(cs, c, &key, &key);
+  }
+  std::atomic<bool> ok{true};
+  auto run = [&](int n) {
+    std::thread server([&] {
+      for (int r = 0; r < n; r++) {
+        for (int i = 0; i < conns; i++)
+          for (int k = 0; k < kRecords; k++)  // one tls_write per 16 KiB record
+            atls_sb_write(ss, sc[i], 23, body.data() + k * kContent, kContent);
+        if (atls_sb_flush(ss) < 0) ok = false;
+      }
+    });
+    std::vector<uint8_t> buf(kContent);
+    for (int r = 0; r < n; r++)
+      for (int i = 0; i < conns; i++)
+        for (int k = 0; k < kRecords; k++) {
+          size_t got = 0;
+          if (atls_sb_read(cs, cc[i], buf.data(), buf.size(), &got) || got != kContent ||
+              std::memcmp(buf.data(), body.data() + k * kContent, kContent))
+            ok = false;
+        }
+    server.join();
+  };
+  run(1);  // warm-up: device buffers, code objects, pinned staging
+  const auto t0 = std::chrono::steady_clock::now();
+  run(reps);
+  const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  std::printf("{\"config\": \"c1_server_https_loopback_1MiB\", \"impl\": \"native atls_stream_batch\", "
+              "\"suite\": \"TLS_AES_128_GCM_SHA256\", \"records_per_body\": %d, \"conns\": %d, \"reps\": %d, "
+              "\"verified\": %s, \"gpu_MBps\": %.1f}\n",
+              kRecords, conns, reps, ok.load() ? "true" : "false", (double)reps * conns * kBody / dt / 1e6);
+  for (int fd : fds) close(fd);
+  atls_sb_destroy(ss);
+  atls_sb_destroy(cs);
+  atls_engine_destroy(es);
+  atls_engine_destroy(ec);
+  return ok.load() ? 0 : 1;
+}
