@@ -235,7 +235,8 @@ long atls_sb_recv(atls_stream_batch* sb, int conn, size_t max_bytes) {
     std::lock_guard<std::mutex> lk(sb->mu);
     fd = sb->conns[(size_t)conn].fd;
   }
-  std::vector<uint8_t> buf(max_bytes);
+  thread_local std::vector<uint8_t> buf;  // reused: a fresh vector would zero max_bytes per call
+  if (buf.size() < max_bytes) buf.resize(max_bytes);
   ssize_t k;
   do {
     k = recv(fd, buf.data(), max_bytes, 0);
@@ -337,7 +338,7 @@ int atls_sb_read(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size
         std::lock_guard<std::mutex> lk(sb->mu);
         fd = sb->conns[(size_t)conn].fd;
       }
-      std::vector<uint8_t> more(size_t(1) << 20);
+      thread_local std::vector<uint8_t> more(size_t(1) << 20);
       for (;;) {
         const ssize_t m = recv(fd, more.data(), more.size(), MSG_DONTWAIT);
         if (m <= 0) break;  // EAGAIN, EOF (seen by the next blocking read) or an error
