@@ -1,6 +1,8 @@
 """Benchmark: device-resident TLS-record AEAD throughput (BASELINE.json metric) on MI355X.
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2_aes128gcm_64Ki_x_16KiB]
+(--config c1_server_https_loopback_1MiB: BASELINE config C1, the loopback through the batched socket
+path, MB/s, with the reference's per-record CPU path as cpu_baseline)
 For N > 1 the driver launches one rank per GPU with torch.distributed.run; each rank seals
 its own pre-sharded, device-resident batch of the config (records are independent, so there
 is no data-path collective: weak scaling). One step = one atls_seal_batch over the whole
@@ -94,8 +96,74 @@ def cpu_baseline(batch, inbuf_host, budget_s, threads):
                        f"{d1} records ({p1} B) in {t1:.1f} s")
 
 
+C1 = "c1_server_https_loopback_1MiB"
+
+
+def c1_cpu_reference(body, reps):
+    """BASELINE config C1's reference path: the oracle's restatement of RecordPayloadProtection
+    (ora_record_seal / ora_record_open, one record per call as tls_write / tls_read do) through
+    the same 127.0.0.1 socket loop as the GPU run (tools/c1_loopback.py). Returns seconds."""
+    import oracle as ora
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import c1_loopback as c1
+
+    rc, key, iv = ora.key_from_secret(32, c1.SECRET, 16, 12)
+    assert rc == 0
+    frags = [body[i * c1.CONTENT:(i + 1) * c1.CONTENT] for i in range(c1.N_REC)]
+
+    def seal_body():
+        parts = []
+        for seq, f in enumerate(frags):
+            rc, wire = ora.record_seal(0x1301, key, iv, seq, 23, f)
+            assert rc == 0
+            parts.append(wire)
+        return b"".join(parts)
+
+    def open_wire(wire):
+        pt, pos = [], 0
+        for seq in range(c1.N_REC):
+            n = (wire[pos + 3] << 8) | wire[pos + 4]
+            rc, frag, ctype = ora.record_open(0x1301, key, iv, seq, wire[pos:pos + 5 + n])
+            assert rc == 0 and ctype == 23
+            pt.append(frag)
+            pos += 5 + n
+        return b"".join(pt)
+
+    dt, pt = c1._loop(seal_body, open_wire, c1.N_REC * (5 + c1.CONTENT + 1 + 16), reps)
+    assert pt == body
+    return dt
+
+
+def run_c1(args):
+    """C1 (server_https over loopback, 1 MiB body of 64 x 16 KiB AES-128-GCM records): the batched
+    socket path on the GPU (tools/c1_loopback.py run_gpu, one WIRE batch per body) against the
+    reference's per-record CPU path over the same loop."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import c1_loopback as c1
+
+    body = np.random.default_rng(0xC1).integers(0, 256, c1.N_REC * c1.CONTENT, dtype=np.uint8).tobytes()
+    dt, pt = c1.run_gpu(body, args.steps)
+    assert pt == body
+    result = {"metric": "MB/s of response body through seal -> 127.0.0.1 socket -> open (server_https loopback)",
+              "value": round(args.steps * len(body) / dt / 1e6, 1), "unit": "MB/s", "n_gpus": 1,
+              "steps": args.steps, "warmup": 1, "ms_per_step": round(dt / args.steps * 1e3, 3),
+              "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u8",
+              "data": "synthetic 1 MiB body, RFC 8448 server traffic secret",
+              "config": {"workload": C1, "records_per_body": c1.N_REC, "record_content": c1.CONTENT,
+                         "suite": "TLS_AES_128_GCM_SHA256", "path": "anothertls_amd.stream.StreamBatch (WIRE mode)"}}
+    if not args.no_cpu_baseline:
+        t = c1_cpu_reference(body, 1)
+        result["cpu_baseline"] = {"value": round(len(body) / t / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+                                  "sample": "one 1 MiB body (64 records) through the same socket loop, oracle "
+                                            "ora_record_seal / ora_record_open per record"}
+    print(json.dumps(result), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == C1:
+        return run_c1(args)
     rank, local, world = dist.env_ranks()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)

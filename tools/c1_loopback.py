@@ -4,15 +4,15 @@ thread seals and writes, the client reads, splits the stream into records and op
 Keys: RFC 8448 §3 server handshake traffic secret -> write key / iv (Key::from_hkdf,
 net/key_schedule.rs:40-50), sequence numbers 0..63.
 
-Two implementations of the same loop, each checked end to end (body and content types):
+The GPU path of the loop, checked end to end (body and content types); the reference's
+per-record CPU path over the same loop is bench.py's cpu_baseline for this config
+(`python bench.py --config c1_server_https_loopback_1MiB`):
   * gpu  — atls_derive_keys, then anothertls_amd.stream.StreamBatch on each side: the writes of
            a body (of every connection, with --conns N) sealed in one WIRE-mode atls_seal_batch
            (the device writes header || ct || tag), the received records opened in one
            atls_open_batch (net/stream.rs:97-150 batched);
-  * cpu  — the reference's per-record path as the oracle restates it (oracle/ref_restatement.c
-           ora_record_seal / ora_record_open, one record per call like tls_write / tls_read).
-Prints one JSON line: MB/s of body through seal -> socket -> open for each.
-python tools/c1_loopback.py [--reps N] [--cpu-only] [--conns N]"""
+Prints one JSON line: MB/s of body through seal -> socket -> open.
+python tools/c1_loopback.py [--reps N] [--conns N]"""
 import argparse
 import json
 import os
@@ -73,35 +73,6 @@ def _loop(seal_body, open_wire, wire_len, reps):
     server.close()
     client.close()
     return dt, out["pt"]
-
-
-def run_cpu(body, reps):
-    import oracle as ora
-
-    rc, key, iv = ora.key_from_secret(32, SECRET, 16, 12)
-    assert rc == 0
-    frags = [body[i * CONTENT:(i + 1) * CONTENT] for i in range(N_REC)]
-
-    def seal_body():
-        parts = []
-        for seq, f in enumerate(frags):
-            rc, wire = ora.record_seal(0x1301, key, iv, seq, 23, f)
-            assert rc == 0
-            parts.append(wire)
-        return b"".join(parts)
-
-    def open_wire(wire):
-        pt, pos = [], 0
-        for seq in range(N_REC):
-            n = (wire[pos + 3] << 8) | wire[pos + 4]
-            rc, frag, ctype = ora.record_open(0x1301, key, iv, seq, wire[pos:pos + 5 + n])
-            assert rc == 0 and ctype == 23
-            pt.append(frag)
-            pos += 5 + n
-        return b"".join(pt)
-
-    wire_len = N_REC * (5 + CONTENT + 1 + 16)
-    return _loop(seal_body, open_wire, wire_len, reps)
 
 
 def _tcp_pairs(n):
@@ -169,22 +140,14 @@ def run_gpu(body, reps, conns=1):
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--reps", type=int, default=8)
-    p.add_argument("--cpu-reps", type=int, default=1)
-    p.add_argument("--cpu-only", action="store_true")
-    p.add_argument("--conns", type=int, default=1, help="GPU path: connections sharing one batch")
+    p.add_argument("--conns", type=int, default=1, help="connections sharing one batch")
     args = p.parse_args()
     body = np.random.default_rng(0xC1).integers(0, 256, N_REC * CONTENT, dtype=np.uint8).tobytes()
-    res = {"config": "c1_server_https_loopback_1MiB", "records": N_REC, "suite": "TLS_AES_128_GCM_SHA256",
-           "body_bytes": len(body)}
-    dt, pt = run_cpu(body, args.cpu_reps)
+    dt, pt = run_gpu(body, args.reps, args.conns)
     assert pt == body
-    res["cpu_reference_MBps"] = round(args.cpu_reps * len(body) / dt / 1e6, 3)
-    if not args.cpu_only:
-        dt, pt = run_gpu(body, args.reps, args.conns)
-        assert pt == body
-        res["gpu_conns"] = args.conns
-        res["gpu_MBps"] = round(args.reps * args.conns * len(body) / dt / 1e6, 1)
-    print(json.dumps(res), flush=True)
+    print(json.dumps({"config": "c1_server_https_loopback_1MiB", "records": N_REC, "suite": "TLS_AES_128_GCM_SHA256",
+                      "body_bytes": len(body), "gpu_conns": args.conns,
+                      "gpu_MBps": round(args.reps * args.conns * len(body) / dt / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
