@@ -254,13 +254,16 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   const uint32_t S = m + 1u;        // slots: E(J0) + GHASH blocks
   const uint32_t in_bytes = len;    // bytes readable from src
 
-  {
+  // A record of one step (S <= 64: AEAD up to 976 B in TLS mode) multiplies nothing by H^64:
+  // Y starts at 0 and the lane combine applies every power, so it skips the table.
+  const bool one_step = S <= 64u;
+  if (!one_step) {
     uint32_t seed[4];
 #pragma unroll
     for (int w = 0; w < 4; w++) seed[w] = k->p4_be[lane >> 1][w];
     if (!(ATLS_DBG_SKIP & 4)) ghash_table_entries<8>(wb, seed, lane >> 1, (lane & 1) * 8);
+    wave_lds_sync();
   }
-  wave_lds_sync();
 
   uint32_t y[4] = {0, 0, 0, 0};
   uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0), lane 0
@@ -431,7 +434,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     }
     // Y <- Y * H^64 ^ B on the lanes that hold a GHASH block; the others keep Y (s_last below).
     uint32_t yn[4] = {y[0], y[1], y[2], y[3]};
-    if (!(ATLS_DBG_SKIP & 8)) ghash_mul<ATLS_GHASH_W>(yn, wb);
+    if (base && !(ATLS_DBG_SKIP & 8)) ghash_mul<ATLS_GHASH_W>(yn, wb);  // Y = 0 before the first step
     if (s >= 1 && s <= m) {
 #pragma unroll
       for (int w = 0; w < 4; w++) y[w] = yn[w] ^ B[w];
