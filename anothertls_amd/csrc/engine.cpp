@@ -34,7 +34,7 @@ extern "C" int atls_launch_aes_blocks(int decrypt, const void* ks, const uint8_t
 extern "C" int atls_launch_key_setup(const atls_key* keys, uint32_t n, void* ks, hipStream_t s);
 extern "C" int atls_launch_plan(int open, const void* ks, const atls_rec* recs, uint32_t n, uint32_t n_slots,
                                 atls_open_result* res, uint32_t* err, void* P, uint8_t* keys, uint32_t* idx,
-                                hipStream_t s);
+                                uint32_t* wg, int cus, hipStream_t s);
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
@@ -80,7 +80,7 @@ struct atls_engine {
   bool has_aes = false, has_chacha = false;  // suites present in the key table: skip idle kernels
   int aes_nr_mask = 0;                       // bit 0/1/2: AES slots with 10/12/14 rounds
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
-  DevBuf plan, plan_keys, plan_idx;          // batch plan (plan.hip)
+  DevBuf plan, plan_keys, plan_idx, plan_wg; // batch plan (plan.hip)
   DevBuf ksbuf, ksok;                        // hybrid batches: keystream of ks_bs.hip
   float hybrid_f = 0.0f;                     // ATLS_HYBRID: share of a direct AES batch keyed on the VALU
   uint32_t hybrid_min = 8192;                // ATLS_HYBRID_MIN: smallest batch that splits
@@ -281,10 +281,11 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   int rc = 0;
   const uint32_t* idx = nullptr;
   if (planned) {
-    if (!e->plan.reserve(sizeof(atls::PlanHdr)) || !e->plan_keys.reserve(n) || !e->plan_idx.reserve(4 * (size_t)n))
+    if (!e->plan.reserve(sizeof(atls::PlanHdr)) || !e->plan_keys.reserve(n) || !e->plan_idx.reserve(4 * (size_t)n) ||
+        !e->plan_wg.reserve(2 * 4 * (size_t)atls::kPlanKeys * atls::kPlanMaxWG))
       return ATLS_INTERNAL_ERROR;
     rc = atls_launch_plan(open, e->ks.p, d_recs, n, e->n_slots, d_res, (uint32_t*)e->err.p, e->plan.p,
-                          (uint8_t*)e->plan_keys.p, (uint32_t*)e->plan_idx.p, s);
+                          (uint8_t*)e->plan_keys.p, (uint32_t*)e->plan_idx.p, (uint32_t*)e->plan_wg.p, e->cus, s);
     if (rc) return rc;
     idx = (const uint32_t*)e->plan_idx.p;
   }
@@ -475,7 +476,7 @@ void atls_engine_destroy(atls_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   for (DevBuf* b : {&e->ksbuf, &e->ksok, &e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
-                    &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx})
+                    &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx, &e->plan_wg})
     b->release();
   if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);
   if (e->ev_side) (void)hipEventDestroy(e->ev_side);
