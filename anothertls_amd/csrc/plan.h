@@ -17,7 +17,7 @@ constexpr uint32_t kKsStride = 8 * kKsUnits;  // AEAD <= 16,848 B
 struct PlanHdr {
   uint32_t off[kPlanLists + 1];                  // list l = idx[off[l] .. off[l+1])
   uint32_t next[kPlanLists];                     // unused
-  uint32_t count[kPlanLists * kPlanClasses];     // records per key (plan_scan)
+  uint32_t count[kPlanLists * kPlanClasses];     // unused
   uint32_t cursor[kPlanLists * kPlanClasses];    // unused
 };
 

@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void plan_count(const atls_rec* recs, uint32_t
 
 // One workgroup: exclusive prefix over the G x 64 histogram entries in key-major order, i.e. list
 // by list, longest class first, workgroup by workgroup. wgoff[k][b] = start of workgroup b's
-// records of key k in idx; P->off[l] = start of list l; P->count[k] = records of key k.
+// records of key k in idx; P->off[l] = start of list l.
 __global__ __launch_bounds__(1024) void plan_scan(const uint32_t* wgcount, uint32_t G, uint32_t* wgoff, PlanHdr* P) {
   __shared__ uint32_t part[1024];
   const uint32_t E = kPlanKeys * G, t = threadIdx.x;
@@ -95,13 +95,7 @@ __global__ __launch_bounds__(1024) void plan_scan(const uint32_t* wgcount, uint3
   }
   uint32_t run = part[t] - sum;
   for (uint32_t e = lo; e < hi; e++) {
-    const uint32_t k = e / G;
-    if (e % G == 0) {
-      if (k % kPlanClasses == 0) P->off[k / kPlanClasses] = run;
-      uint32_t c = 0;
-      for (uint32_t b = 0; b < G; b++) c += wgcount[k * G + b];
-      P->count[k] = c;
-    }
+    if (e % (G * kPlanClasses) == 0) P->off[e / (G * kPlanClasses)] = run;
     wgoff[e] = run;
     run += wgcount[e];
   }
