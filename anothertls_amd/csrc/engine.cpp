@@ -85,6 +85,7 @@ struct atls_engine {
   float hybrid_f = 0.0f;                     // ATLS_HYBRID: share of a direct AES batch keyed on the VALU
   uint32_t hybrid_min = 8192;                // ATLS_HYBRID_MIN: smallest batch that splits
   int hybrid_wgs = 2;                        // ATLS_HYBRID_WGS: keystream workgroups per CU
+  int chacha_wgs = 8;                        // ATLS_CHACHA_WGS: ChaCha20-Poly1305 workgroups per CU
   bool force_plan = false;                   // ATLS_FORCE_PLAN=1: plan every batch (tests)
   bool no_pipeline = false;                  // ATLS_NO_PIPELINE=1: stage host batches in one piece
   std::mutex mu;
@@ -132,7 +133,7 @@ int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n
   // direct batches only (one record kernel in the key table)
   if (e->has_chacha)
     return atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, nullptr,
-                              e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * 8, s);
+                              e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s);
   return atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, nullptr, e->plan.p, (uint32_t*)e->err.p, e->n_slots,
                          e->aes_nr_mask, e->cus, s);
@@ -149,7 +150,11 @@ int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n
 int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
                        void* out, uint8_t* tags_out, const uint8_t* tags_in, atls_open_result* res,
                        size_t in_end, size_t out_end, size_t aux_end) {
-  constexpr size_t kChunkBytes = 32u << 20;
+  static const size_t kChunkBytes = [] {  // ATLS_CHUNK_MB overrides (tuning)
+    const char* v = std::getenv("ATLS_CHUNK_MB");
+    const long mb = v ? std::atol(v) : 32;
+    return (size_t)(mb > 0 ? mb : 32) << 20;
+  }();
   auto ilen = [&](const atls_rec& r) { return rec_in_len(r, open); };
   auto olen = [&](const atls_rec& r) { return rec_out_len(r, open); };
   for (uint32_t i = 1; i < n; i++)
@@ -300,7 +305,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
       cs = e->stream2;
     }
     rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, idx,
-                            e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * 8, cs);
+                            e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs);
     if (rc) return rc;
     if (side && hipEventRecord(e->ev_side, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
@@ -462,6 +467,7 @@ atls_engine* atls_engine_create(int device) {
   if (const char* v = std::getenv("ATLS_HYBRID")) e->hybrid_f = std::min(0.9f, std::max(0.0f, (float)std::atof(v)));
   if (const char* v = std::getenv("ATLS_HYBRID_MIN")) e->hybrid_min = (uint32_t)std::atoi(v);
   if (const char* v = std::getenv("ATLS_HYBRID_WGS")) e->hybrid_wgs = std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("ATLS_CHACHA_WGS")) e->chacha_wgs = std::max(1, std::atoi(v));
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
       hipStreamSynchronize(e->stream) != hipSuccess) {
     atls_engine_destroy(e);
