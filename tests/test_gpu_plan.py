@@ -96,3 +96,43 @@ def test_rejected_records_device_descriptors(atls, planned):
     others = np.setdiff1d(np.arange(n), [3, 9])
     assert (res["status"][others] == atls.TlsError.DECRYPT_ERROR).all()
     eng.close()
+
+
+def test_plan_large_batch_many_workgroups(atls):
+    """A mixed batch large enough that every plan workgroup strides over several chunks of
+    records (300 Ki records, 512 workgroups): every record lands in its list exactly once,
+    longest class first, and sampled records seal as the oracle does."""
+    import oracle as ora
+    from anothertls_amd import workload
+
+    rng = np.random.default_rng(17)
+    n = 300 * 1024
+    lens = rng.integers(0, 2048, n).astype(np.uint64)
+    b = workload.tls_batch(n, lens, lambda k: np.where(np.arange(k) % 2 == 0, 0x1301, 0x1303).astype(np.uint16),
+                           n_keys=64)
+    recs = b["recs"]
+    eng = atls.Engine(0)
+    eng.set_keys(b["keys"])
+    inbuf = rng.integers(0, 256, b["in_bytes"] + 16, dtype=np.uint8)
+    out = np.zeros(b["out_bytes"] + 16, np.uint8)
+    tags = np.zeros(16 * n, np.uint8)
+    eng.seal_batch(recs, inbuf, np.zeros(16, np.uint8), out, tags)
+    off, idx = _plan(atls, eng, n)
+    assert off[4] == n
+    aes = np.flatnonzero(recs["key_slot"] % 2 == 0)
+    for lst, members in ((0, aes), (3, np.setdiff1d(np.arange(n), aes))):
+        got = idx[off[lst]:off[lst + 1]]
+        assert np.array_equal(np.sort(got), members), lst
+        cls = np.minimum(recs["len"][got] >> 10, 15)
+        assert (np.diff(cls.astype(np.int64)) <= 0).all()
+    sample = np.sort(rng.choice(n, 512, replace=False))
+    okeys = (ora.OraKey * len(b["keys"])).from_buffer_copy(b["keys"].tobytes())
+    srecs = recs[sample].copy()
+    orecs = (ora.OraRec * len(srecs)).from_buffer_copy(srecs.tobytes())
+    oout, otags = np.zeros_like(out), np.zeros(16 * len(srecs), np.uint8)
+    assert ora.seal_batch(okeys, orecs, inbuf, np.zeros(16, np.uint8), oout, otags, 8) == 0
+    for j, i in enumerate(sample):
+        o, L = int(recs["out_off"][i]), int(recs["len"][i]) + 1
+        assert np.array_equal(out[o:o + L], oout[o:o + L]), i
+        assert np.array_equal(tags[16 * i:16 * i + 16], otags[16 * j:16 * j + 16]), i
+    eng.close()
