@@ -5,7 +5,7 @@
 // the last 64-byte block unencrypted when len % 64 == 0 (cipher.rs:99-102), and the tag is
 // computed over that output. Record framing as in net/record.rs:162-240.
 //
-// Mapping: a group of G = 16 lanes per record (4 records per wavefront). Slot j of a record
+// Mapping: a group of G lanes per record (G = 16, or 4 for short records, chacha_kernel). Slot j of a record
 // is ChaCha20 block counter j: slot 0 = Poly1305 key generation (poly1305.rs:19-22) plus the
 // AAD blocks, slot j >= 1 = bytes [64(j-1), 64j) of the record (counter starts at 1,
 // poly1305.rs:77). Lane l of the group owns slots j = l (mod 16): each step the group reads and
@@ -19,7 +19,9 @@
 
 namespace atls {
 
-constexpr int G = 16;           // lanes per record
+#ifndef ATLS_CHACHA_SHORT
+#define ATLS_CHACHA_SHORT 4096  // records up to this length take 4 lanes each, longer ones 16
+#endif
 constexpr uint32_t M26 = 0x3ffffffu;
 
 struct P130 { uint32_t l[5]; };
@@ -88,6 +90,7 @@ __device__ __forceinline__ void p_finish(P130 h, const uint32_t s[4], uint32_t t
   f = (uint64_t)w3 + s[3] + (f >> 32); t[3] = (uint32_t)f;
 }
 
+template <int G>
 __device__ __forceinline__ P130 shfl_p(const P130& v, int src) {
   P130 o;
   for (int i = 0; i < 5; i++) o.l[i] = __shfl(v.l[i], src, G);
@@ -131,9 +134,11 @@ struct ChArgs {
   PlanHdr* plan;
   uint32_t* err;        // direct mode: sticky error word
   uint32_t n_slots;     // direct mode: key-table size
+  const uint32_t* wgmax;  // direct mode: per-workgroup longest record (batch_prep), or nullptr
+  uint32_t n_wgmax;
 };
 
-template <bool OPEN>
+template <bool OPEN, int G>
 __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl) {
   // TLS and WIRE: nonce from (static IV, seq), 5-byte AAD; WIRE also frames the record
   const bool wire = d.mode == ATLS_MODE_WIRE;
@@ -209,7 +214,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         const P130 m = p_mul(R, t);
         if (gl >= d) R = m;
       }
-      r64 = shfl_p(R, G - 1);
+      r64 = shfl_p<G>(R, G - 1);
     }
     if (!active) continue;
 
@@ -327,7 +332,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       const uint32_t e = Q - ref;  // 1..65
       // r^e = r^(e mod 4) * (r^4)^(e >> 2); (r^4)^u is lane u-1's R
       const uint32_t u = e >> 2, c = e & 3u;
-      P130 ru = shfl_p(R, (int)(u ? u - 1u : 0u));
+      P130 ru = shfl_p<G>(R, (int)(u ? u - 1u : 0u));
       if (u == 0) { ru = p_zero(); ru.l[0] = 1; }
       P130 pw;
       if (c == 0) pw = ru;
@@ -389,54 +394,74 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   }
 }
 
-// The waves take the ChaCha20-Poly1305 work list (plan.hip, longest first) round-robin, 4
-// consecutive positions (records of similar length) per wave and step, one per 16-lane group.
-template <bool OPEN>
+// One group of G lanes seals / opens the record at work-list position q (direct batches: the
+// kernel validates the descriptor itself).
+template <bool OPEN, int G>
+__device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W, uint32_t q, uint32_t cnt, int gl) {
+  if (q >= cnt) return;
+  const uint32_t r = W.record(q);
+  const atls_rec d = A.recs[r];
+  const uint32_t st = A.idx ? 0u : direct_reject(d, A.ks, A.n_slots);  // direct mode
+  if (st) {
+    if (gl == 0) {
+      atomicOr(A.err, 1u);
+      if (OPEN) {
+        atls_open_result rr = {0, (uint8_t)st, 0, {0, 0}};
+        A.res[r] = rr;
+      }
+    }
+  } else {
+    chacha_record<OPEN, G>(A, d, A.ks + d.key_slot, r, gl);
+  }
+}
+
+// G = 16: the waves take the work list (plan.hip, longest first; or the batch itself)
+// round-robin, 4 consecutive positions per wave and step, one per 16-lane group.
+// G = 4 (batches whose records are all short, ATLS_CHACHA_SHORT): 16 positions per wave and step,
+// one per 4-lane group: the per-record Poly1305 set-up (r powers, lane scan, combine) is shared
+// by 4 lanes instead of 16, and a 1.5 KiB record's 26 ChaCha blocks fill 28 lane-slots instead
+// of 32 (C3: 690 -> 906 GiB/s). Direct batches launch both kernels after batch_prep (plan.hip)
+// has recorded the longest record; each kernel reads it and only the matching one does the work.
+// Planned batches (mixed lengths) launch G = 16 only.
+template <bool OPEN, int G>
 __global__ __launch_bounds__(256) void chacha_kernel(ChArgs A) {
   const int lane = threadIdx.x & 63;
-  const int gl = lane & (G - 1);
-  const uint32_t grp = (uint32_t)(lane / G);
+  if (A.wgmax) {
+    uint32_t mx = 0;
+    for (uint32_t i = (uint32_t)lane; i < A.n_wgmax; i += 64) mx = max(mx, A.wgmax[i]);
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    if ((mx <= (uint32_t)ATLS_CHACHA_SHORT) != (G == 4)) return;  // the other kernel's batch
+  }
   const WorkList W{A.idx, A.plan, kListChacha, A.n};
   const uint32_t cnt = W.size();
   constexpr uint32_t kPer = 64u / G;
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
   const uint32_t stride = gridDim.x * blockDim.x / 64u * kPer;
-  for (uint32_t q0 = wave * kPer; q0 < cnt; q0 += stride) {
-    const uint32_t q = q0 + grp;
-    if (q < cnt) {
-      const uint32_t r = W.record(q);
-      const atls_rec d = A.recs[r];
-      const uint32_t st = A.idx ? 0u : direct_reject(d, A.ks, A.n_slots);  // direct mode
-      if (st) {
-        if (gl == 0) {
-          atomicOr(A.err, 1u);
-          if (OPEN) {
-            atls_open_result rr = {0, (uint8_t)st, 0, {0, 0}};
-            A.res[r] = rr;
-          }
-        }
-      } else {
-        chacha_record<OPEN>(A, d, A.ks + d.key_slot, r, gl);
-      }
-    }
-  }
+  for (uint32_t q0 = wave * kPer; q0 < cnt; q0 += stride)
+    chacha_group<OPEN, G>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
 }
 
 }  // namespace atls
 
+// wgmax / n_wgmax: batch_prep's per-workgroup longest record for a direct batch (both kernel
+// widths are launched, the matching one works), nullptr for a planned batch (G = 16 only).
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
-                                  uint32_t n_slots, int grid, hipStream_t s) {
+                                  uint32_t n_slots, const uint32_t* wgmax, uint32_t n_wgmax, int grid, hipStream_t s) {
   if (n == 0) return 0;
   atls::ChArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, idx,
-                 (atls::PlanHdr*)plan, err, n_slots};
-  const uint32_t per_block = 256 / atls::G;
-  uint32_t want = (n + per_block - 1) / per_block;
-  uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
-  if (open)
-    hipLaunchKernelGGL(atls::chacha_kernel<true>, dim3(g), dim3(256), 0, s, A);
-  else
-    hipLaunchKernelGGL(atls::chacha_kernel<false>, dim3(g), dim3(256), 0, s, A);
+                 (atls::PlanHdr*)plan, err, n_slots, wgmax, n_wgmax};
+  const uint32_t want16 = (n + 15u) / 16u, want4 = (n + 63u) / 64u;  // 4 waves x 4 / x 16 positions
+  const uint32_t g16 = (uint32_t)grid < want16 ? (uint32_t)grid : want16;
+  const uint32_t g4 = (uint32_t)grid < want4 ? (uint32_t)grid : want4;
+  if (open) {
+    hipLaunchKernelGGL((atls::chacha_kernel<true, 16>), dim3(g16), dim3(256), 0, s, A);
+    if (wgmax) hipLaunchKernelGGL((atls::chacha_kernel<true, 4>), dim3(g4), dim3(256), 0, s, A);
+  } else {
+    hipLaunchKernelGGL((atls::chacha_kernel<false, 16>), dim3(g16), dim3(256), 0, s, A);
+    if (wgmax) hipLaunchKernelGGL((atls::chacha_kernel<false, 4>), dim3(g4), dim3(256), 0, s, A);
+  }
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }

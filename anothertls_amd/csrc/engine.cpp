@@ -42,7 +42,9 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
-                                  uint32_t n_slots, int grid, hipStream_t s);
+                                  uint32_t n_slots, const uint32_t* wgmax, uint32_t n_wgmax, int grid, hipStream_t s);
+extern "C" int atls_launch_prep(const atls_rec* recs, uint32_t n, uint32_t* err, uint32_t* wgmax, hipStream_t s,
+                                uint32_t* n_wg);
 extern "C" int atls_launch_derive(uint16_t suite, const uint8_t* secrets, uint32_t secret_len, uint32_t n,
                                   atls_key* out, hipStream_t s);
 
@@ -81,6 +83,7 @@ struct atls_engine {
   int aes_nr_mask = 0;                       // bit 0/1/2: AES slots with 10/12/14 rounds
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
   DevBuf plan, plan_keys, plan_idx, plan_wg; // batch plan (plan.hip)
+  DevBuf wgmax;                              // batch_prep: per-workgroup longest record
   DevBuf ksbuf, ksok;                        // hybrid batches: keystream of ks_bs.hip
   float hybrid_f = 0.0f;                     // ATLS_HYBRID: share of a direct AES batch keyed on the VALU
   uint32_t hybrid_min = 8192;                // ATLS_HYBRID_MIN: smallest batch that splits
@@ -129,11 +132,16 @@ void extents(const atls_rec* recs, uint32_t n, bool open, size_t* in_end, size_t
 
 int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n, const uint8_t* d_in,
                    const uint8_t* d_aux, uint8_t* d_out, uint8_t* d_tags_out, const uint8_t* d_tags_in,
-                   atls_open_result* d_res, hipStream_t s) {
-  // direct batches only (one record kernel in the key table)
-  if (e->has_chacha)
+                   atls_open_result* d_res, hipStream_t s, int slot) {
+  // direct batches only (one record kernel in the key table); slot: which half of the wgmax
+  // scratch this launch uses (the host pipeline's two streams run chunks concurrently)
+  if (e->has_chacha) {
+    uint32_t n_wg = 0;
+    uint32_t* wgmax = (uint32_t*)e->wgmax.p + 256 * slot;
+    if (atls_launch_prep(d_recs, n, nullptr, wgmax, s, &n_wg)) return ATLS_INTERNAL_ERROR;  // err stays sticky
     return atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, nullptr,
-                              e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s);
+                              e->plan.p, (uint32_t*)e->err.p, e->n_slots, wgmax, n_wg, e->cus * e->chacha_wgs, s);
+  }
   return atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, nullptr, e->plan.p, (uint32_t*)e->err.p, e->n_slots,
                          e->aes_nr_mask, e->cus, s);
@@ -196,7 +204,7 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
         hipMemcpyAsync(d_out + out_lo, (uint8_t*)out + out_lo, out_hi - out_lo, hipMemcpyHostToDevice, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     int rc = launch_records(e, open, d_recs + a, cnt, d_in, (const uint8_t*)e->aux.p, d_out, d_tags + 16 * (size_t)a,
-                            d_tags + 16 * (size_t)a, d_res + a, s);
+                            d_tags + 16 * (size_t)a, d_res + a, s, c);
     if (rc) return rc;
     if (pitched) {
       if (width && hipMemcpy2DAsync((uint8_t*)out + out_lo, pitch, d_out + out_lo, pitch, width, cnt,
@@ -261,7 +269,8 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   if (!dev_ptrs) {
     extents(recs, n, open, &in_end, &out_end, &aux_end);
     if (!e->in.reserve(in_end + 16) || !e->out.reserve(out_end + 16) || !e->aux.reserve(aux_end + 16) ||
-        !e->tags.reserve(16 * (size_t)n) || !e->res.reserve(sizeof(atls_open_result) * (size_t)n))
+        !e->tags.reserve(16 * (size_t)n) || !e->res.reserve(sizeof(atls_open_result) * (size_t)n) ||
+        !e->wgmax.reserve(4 * 512))
       return ATLS_INTERNAL_ERROR;
     if (!planned && n > 1 && !e->no_pipeline) {
       const int rc = run_host_pipelined(e, open, recs, n, in, aux, out, tags_out, tags_in, res, in_end, out_end, aux_end);
@@ -282,7 +291,17 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     d_tags_in = (const uint8_t*)e->tags.p;
     d_res = (atls_open_result*)e->res.p;
   }
-  if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  // Direct ChaCha batches: batch_prep clears err and records the longest record, from which the
+  // ChaCha kernels pick their lane width (chacha.hip); everything else: a memset of err.
+  uint32_t n_wgmax = 0;
+  const bool prep = !planned && e->has_chacha;
+  if (prep) {
+    if (!e->wgmax.reserve(4 * 512) ||
+        atls_launch_prep(d_recs, n, (uint32_t*)e->err.p, (uint32_t*)e->wgmax.p, s, &n_wgmax))
+      return ATLS_INTERNAL_ERROR;
+  } else if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess) {
+    return ATLS_INTERNAL_ERROR;
+  }
   int rc = 0;
   const uint32_t* idx = nullptr;
   if (planned) {
@@ -305,7 +324,8 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
       cs = e->stream2;
     }
     rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, idx,
-                            e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs);
+                            e->plan.p, (uint32_t*)e->err.p, e->n_slots, prep ? (const uint32_t*)e->wgmax.p : nullptr,
+                            n_wgmax, e->cus * e->chacha_wgs, cs);
     if (rc) return rc;
     if (side && hipEventRecord(e->ev_side, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
@@ -482,7 +502,7 @@ void atls_engine_destroy(atls_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   for (DevBuf* b : {&e->ksbuf, &e->ksok, &e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
-                    &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx, &e->plan_wg})
+                    &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx, &e->plan_wg, &e->wgmax})
     b->release();
   if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);
   if (e->ev_side) (void)hipEventDestroy(e->ev_side);

@@ -1,0 +1,58 @@
+"""GPU: the two ChaCha20-Poly1305 lane widths (chacha.hip). A direct batch whose records are all
+short (<= ATLS_CHACHA_SHORT = 4096 B) runs 4 lanes per record, any other batch 16; both are
+checked against the oracle on the lengths that exercise the per-lane Poly1305 combine and the
+reference's F4 quirk (ChaCha20::encrypt leaves the last block unencrypted when len % 64 == 0,
+crypto/chacha20/cipher.rs:99-102), sealed and reopened, with tampered tags."""
+import numpy as np
+import pytest
+
+import oracle as ora
+
+pytestmark = pytest.mark.gpu
+
+SHORT = [0, 1, 15, 16, 17, 62, 63, 64, 65, 127, 128, 191, 255, 256, 1000, 1023, 1024, 1535, 1536, 2047, 4095, 4096]
+
+
+@pytest.fixture(scope="module")
+def atls():
+    import anothertls_amd as a
+
+    if not a.device_available():
+        pytest.skip("no HIP device")
+    return a
+
+
+@pytest.mark.parametrize("lens", [SHORT * 20, SHORT * 20 + [16384]], ids=["all-short-4-lanes", "one-long-16-lanes"])
+def test_chacha_widths_vs_oracle(atls, lens):
+    from anothertls_amd import workload
+
+    lens = np.array(lens, np.uint64)
+    n = len(lens)
+    b = workload.tls_batch(n, lens, 0x1303, n_keys=7)
+    recs = b["recs"]
+    rng = np.random.default_rng(n)
+    inbuf = rng.integers(0, 256, b["in_bytes"] + 16, dtype=np.uint8)
+    eng = atls.Engine(0)
+    eng.set_keys(b["keys"])
+    out = np.zeros(b["out_bytes"] + 16, np.uint8)
+    tags = np.zeros(16 * n, np.uint8)
+    eng.seal_batch(recs, inbuf, np.zeros(16, np.uint8), out, tags)
+    okeys = (ora.OraKey * len(b["keys"])).from_buffer_copy(b["keys"].tobytes())
+    orecs = (ora.OraRec * n).from_buffer_copy(recs.tobytes())
+    oout, otags = np.zeros_like(out), np.zeros_like(tags)
+    assert ora.seal_batch(okeys, orecs, inbuf, np.zeros(16, np.uint8), oout, otags, 8) == 0
+    assert np.array_equal(out, oout) and np.array_equal(tags, otags)
+    r2 = recs.copy()
+    r2["in_off"], r2["len"] = recs["out_off"], recs["len"] + 1
+    bad = tags.copy()
+    bad[16 * np.arange(0, n, 5) + 7] ^= 0x40
+    pt = np.zeros_like(out)
+    res = np.zeros(n, atls.OPEN_RESULT_DTYPE)
+    eng.open_batch(r2, out, np.zeros(16, np.uint8), bad, pt, res)
+    tampered = np.arange(n) % 5 == 0
+    assert (res["status"][tampered] == 50).all() and (res["status"][~tampered] == 0).all()
+    assert (res["content_len"][~tampered] == recs["len"][~tampered]).all()
+    for i in np.flatnonzero(~tampered)[::7]:
+        o, io, L = int(r2["out_off"][i]), int(recs["in_off"][i]), int(recs["len"][i])
+        assert np.array_equal(pt[o:o + L], inbuf[io:io + L]), i
+    eng.close()
