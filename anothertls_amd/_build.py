@@ -39,6 +39,7 @@ def build(force=False, verbose=False, defines=(), out=None):
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(max_workers=min(len(cmds), os.cpu_count() or 1, 8)) as pool:
         list(pool.map(subprocess.check_call, cmds))
+    os.makedirs(os.path.dirname(os.path.abspath(lib)), exist_ok=True)
     tmp = lib + ".tmp"
     subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs])
     os.replace(tmp, lib)

@@ -35,12 +35,16 @@ namespace atls {
 #ifndef ATLS_CTR_CACHE
 #define ATLS_CTR_CACHE 1
 #endif
+#ifndef ATLS_DBG_SHARED_GHASH
+#define ATLS_DBG_SHARED_GHASH 0  // timing experiment only (wrong tags): one GHASH table per workgroup,
+                                 // 16 waves per CU, to price the residency a per-key table would buy
+#endif
 // LDS: AES tables first, row x = 256 B = {T0[x] x32 banks | T1[x] x32 banks} (64 KiB), then one
 // 8 KiB GHASH table per wave.
 // Lane l reads bank (l & 31): conflict-free ds_read_b32.
 constexpr int kTabBytes = 65536;
 constexpr int kGhashBytes = 8192;
-constexpr size_t lds_bytes(int waves) { return kTabBytes + (size_t)waves * kGhashBytes; }
+constexpr size_t lds_bytes(int waves) { return kTabBytes + (size_t)(ATLS_DBG_SHARED_GHASH ? 1 : waves) * kGhashBytes; }
 
 template <int W>
 __device__ __forceinline__ void ghash_mul(uint32_t (&y)[4], uint32_t wb) {
@@ -510,7 +514,7 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   __syncthreads();
   const int wave = (int)uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t lb = 4u * (uint32_t)(lane & 31);
-  const uint32_t wb = (uint32_t)kTabBytes + (uint32_t)wave * kGhashBytes;
+  const uint32_t wb = (uint32_t)kTabBytes + (ATLS_DBG_SHARED_GHASH ? 0u : (uint32_t)wave * kGhashBytes);
   const WorkList W{A.idx, A.plan, NR == 10 ? kListGcm10 : NR == 12 ? kListGcm12 : kListGcm14, A.n};
   const uint32_t cnt = uni(W.size());
   const uint32_t stride = gridDim.x * kWaves;
@@ -553,6 +557,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;
+    if (ATLS_DBG_SHARED_GHASH && w == 16) return 16;
     return (w == 4 || w == 8 || w == 12) ? w : 12;
   }();
   uint32_t want = (n + waves - 1) / waves;
@@ -569,6 +574,9 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
     if (nr_mask & 4) { ATLS_LAUNCH_NR(W, 14) }         \
   }
   ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(12)
+#if ATLS_DBG_SHARED_GHASH
+  ATLS_LAUNCH(16)
+#endif
 #undef ATLS_LAUNCH
 #undef ATLS_LAUNCH_NR
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
