@@ -41,6 +41,14 @@ __device__ __forceinline__ v4u32 lds_u4(uint32_t byte_addr) {
 // p) * H^e, raw words, p = 2*byte + (low nibble ? 1 : 0) covering x^(4p)..x^(4p+3) (n's bit 3
 // is x^(4p)). A position's 16 entries x 16 B fill exactly one 256-B bank row, so lookups never
 // bank-conflict. This writes entries n0 .. n0+CNT-1 of position p from seed = x^(4p) * H^e.
+// ATLS_GHASH_ROT (CNT = 8, lane = 2p + n0/8, the caller's layout): write j of a lane stores
+// entry n0 + ((j + lane) & 7). A ds_write_b128 serves lanes in groups of 8 with bank (a/4) mod
+// 32; in entry order all 8 hit one 16-B bank quad (8-way, 6 % of the GCM kernel's LDS cycles),
+// rotated they hit 8 different quads. Off by default: conflict-free but no faster,
+// and the run-time entry index adds 2.4 % VALU instructions.
+#ifndef ATLS_GHASH_ROT
+#define ATLS_GHASH_ROT 0
+#endif
 template <int CNT>
 __device__ __forceinline__ void ghash_table_entries(uint32_t wb, const uint32_t (&seed_be)[4], int p, int n0) {
   uint32_t P0[4], P1[4], P2[4], P3[4];
@@ -62,7 +70,7 @@ __device__ __forceinline__ void ghash_table_entries(uint32_t wb, const uint32_t 
   }
 #pragma unroll
   for (int j = 0; j < CNT; j++) {
-    const int nv = n0 + j;
+    const int nv = (ATLS_GHASH_ROT && CNT == 8) ? n0 + ((j + 2 * p + (n0 >> 3)) & 7) : n0 + j;
     uint32_t e[4];
 #pragma unroll
     for (int w = 0; w < 4; w++)
