@@ -72,6 +72,44 @@ def seal(kind, key, iv, pt, aad=b""):
         lib.EVP_CIPHER_CTX_free(ctx)
 
 
+_XC = None
+
+
+def _xcheck():
+    """tests/native/build/libxcheck.so (OpenSSL batch sealer; built by `make -C tests/native`)."""
+    global _XC
+    if _XC is None:
+        import os
+        import subprocess
+
+        here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+        path = os.path.join(here, "build", "libxcheck.so")
+        if not os.path.exists(path):
+            subprocess.check_call(["make", "-s", "-C", here])
+        _XC = ctypes.CDLL(path)
+        _XC.xc_seal_tls_batch.argtypes = [ctypes.c_void_p] * 2 + [ctypes.c_uint32] + [ctypes.c_void_p] * 4 + \
+            [ctypes.c_int]
+    return _XC
+
+
+def seal_tls_batch(keys, recs, inbuf, out_bytes, nthreads=16):
+    """OpenSSL seal of every TLS-mode record of a batch (numpy KEY_DTYPE / REC_DTYPE arrays,
+    inbuf a uint8 array). Returns (out, tags, skipped): skipped[i] = 1 for ChaCha20-Poly1305
+    records that hit the reference's last-block quirk, which OpenSSL cannot check."""
+    import numpy as np
+
+    keys = np.ascontiguousarray(keys)
+    recs = np.ascontiguousarray(recs)
+    inbuf = np.ascontiguousarray(inbuf)
+    out = np.zeros(max(out_bytes, 16), np.uint8)
+    tags = np.zeros(16 * len(recs), np.uint8)
+    skipped = np.zeros(max(len(recs), 1), np.uint8)
+    rc = _xcheck().xc_seal_tls_batch(keys.ctypes.data, recs.ctypes.data, len(recs), inbuf.ctypes.data,
+                                     out.ctypes.data, tags.ctypes.data, skipped.ctypes.data, nthreads)
+    assert rc == 0, "OpenSSL batch seal failed"
+    return out, tags, skipped[:len(recs)]
+
+
 def open_(kind, key, iv, ct, aad, tag):
     """Returns plaintext or None on authentication failure."""
     lib = _load()
