@@ -22,6 +22,7 @@
 #include <cstdlib>
 
 #include "gcm_common.h"
+#include "aes_bs.h"
 
 namespace atls {
 
@@ -167,6 +168,68 @@ __device__ __forceinline__ void aes_ctr_r12(uint32_t (&s)[4], uint32_t addr1, co
 }
 #undef TA
 
+// ---- bitsliced steps (VALU) -------------------------------------------------------------------
+// The T-table rounds above are bound by the LDS (one ds_read_b32 per state byte and round) while
+// the VALU is about half idle. A bitsliced step does the AES of up to 8 consecutive fast steps of a
+// record at once with logic only (aes_bs.h: 8 counter blocks per lane, the blocks of slots
+// s, s + 64, ..., s + 448, so every load and store stays a coalesced 1 KiB run per wave); the XOR,
+// store and GHASH of each of those steps follow as in a fast step. Every wave mixes the two kinds
+// of steps within each record, so a CU always has LDS-bound and VALU-bound waves side by side.
+// Round keys come as bit masks from the key schedule (KeySched::bsm): wave-uniform scalar loads.
+template <int NR, bool OPEN>
+__device__ __forceinline__ void bs_steps(uint32_t base, uint32_t k, uint32_t na, const uint32_t (&nraw)[3], uint32_t ctr0,
+                                         const KeySched* ks, const uint8_t* src, uint8_t* dst, uint32_t (&y)[4],
+                                         int64_t& lastnz, bool tls, uint32_t wb, int lane) {
+  // data of this lane's k slots base + lane + 64 i: issued first, they land under the AES rounds
+  uint4 P[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if ((uint32_t)i < k) P[i] = ld16(src + (base + 64u * i + (uint32_t)lane - 1u - na) * 16u);
+  // x[8c + b] = raw word c of the counter block of slot base + lane + 64 b (counter ctr0 + 64 b)
+  uint32_t x[32];
+#pragma unroll
+  for (int b = 0; b < 8; b++) {
+    x[b] = nraw[0];
+    x[8 + b] = nraw[1];
+    x[16 + b] = nraw[2];
+    x[24 + b] = bswap32(ctr0 + 64u * (uint32_t)b);
+  }
+  atls_bs::StateG<1> st;
+  atls_bs::blocks_to_group(x, st[0]);
+  const auto* bsm = cptr(&ks->bsm[0][0]);
+  {
+    atls_bs::Masks m;
+#pragma unroll
+    for (int q = 0; q < 32; q++) m[q >> 3][q & 7] = bsm[q];
+    atls_bs::add_round_key<1>(st, m);
+  }
+#pragma unroll 1
+  for (int rd = 1; rd <= NR; rd++) {
+    atls_bs::sub_bytes<1>(st);
+    atls_bs::Masks m;
+#pragma unroll
+    for (int q = 0; q < 32; q++) m[q >> 3][q & 7] = bsm[32 * rd + q];
+    if (rd < NR) atls_bs::shift_mix_ark<1>(st, m);
+    else atls_bs::shift_ark<1>(st, m);
+  }
+  atls_bs::group_to_blocks(st[0], x);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if ((uint32_t)i >= k) break;
+    const uint32_t off = (base + 64u * i + (uint32_t)lane - 1u - na) * 16u;
+    const v4u32 C = {P[i].x ^ x[i], P[i].y ^ x[8 + i], P[i].z ^ x[16 + i], P[i].w ^ x[24 + i]};
+    st16(dst + off, make_uint4(C.x, C.y, C.z, C.w));
+    if (OPEN && tls) {
+      const uint32_t cw[4] = {C.x, C.y, C.z, C.w};
+      const int j = last_nonzero(cw, 16);
+      if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((cw[j >> 2] >> (8 * (j & 3))) & 0xffu);
+    }
+    ghash_mul<ATLS_GHASH_W>(y, wb);
+    if (OPEN) { y[0] ^= P[i].x; y[1] ^= P[i].y; y[2] ^= P[i].z; y[3] ^= P[i].w; }
+    else { y[0] ^= C.x; y[1] ^= C.y; y[2] ^= C.z; y[3] ^= C.w; }
+  }
+}
+
 // Phase timing (build with -DATLS_TT_STAMPS): shader-clock totals over all records, read back with
 // atls_debug_tt_stamps(). 0 setup (tables, counter cache), 1 fast steps, 2 general steps,
 // 3 lane combine + tag, 4 records, 5 fast steps, 6 general steps.
@@ -177,9 +240,9 @@ __device__ unsigned long long g_tt_stamps[8];
 #define TT_STAMP(var)
 #endif
 
-template <int NR, bool OPEN, bool KS>
+template <int NR, bool OPEN, bool KS, bool BS>
 __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx,
-                           uint32_t lb, uint32_t wb, int lane) {
+                           uint32_t lb, uint32_t wb, int lane, uint32_t phase) {
   TT_STAMP(t_start);
 #ifdef ATLS_TT_STAMPS
   uint64_t t_fast = 0, t_gen = 0, n_fast = 0, n_gen = 0;
@@ -307,11 +370,28 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   else if ((uint32_t)lane <= m) s_last = (int64_t)lane + (int64_t)((m - (uint32_t)lane) / 64) * 64;
   const uint32_t e_comb = s_last >= 1 ? S - (uint32_t)s_last : 1u;  // 1..64
 
+  // Bitsliced steps (BS kernels): up to A.bs_max of the record's F fast steps, as one window of
+  // consecutive steps whose place in the record depends on the wave (phase 0 / 1 / 2: first /
+  // middle / last), so that the waves of a SIMD are rarely in the same kind of step.
+  const uint32_t n_fast = fast_end >= 128u ? (fast_end - 64u) / 64u : 0u;
+  const uint32_t n_bs = (BS && is96 && !use_ks) ? min(A.bs_max, n_fast) : 0u;
+  const uint32_t bs_w0 = (n_fast - n_bs) * phase / 2u;
+
   TT_STAMP(t_setup);
   for (uint32_t base = 0; base < S; base += 64) {
     TT_STAMP(t_step);
     const uint32_t s = base + (uint32_t)lane;
     if (base >= 64u && base + 64u <= fast_end) {  // wave-uniform
+      if (BS && n_bs) {
+        const uint32_t fi = base / 64u - 1u;
+        if (fi >= bs_w0 && fi < bs_w0 + n_bs) {
+          const uint32_t kk = min(8u, bs_w0 + n_bs - fi);
+          bs_steps<NR, OPEN>(base, kk, na, nraw, j0[3] + base + (uint32_t)lane - na, k, src, dst, y, lastnz, tls, wb,
+                             lane);
+          base += 64u * (kk - 1u);
+          continue;
+        }
+      }
       const uint32_t off = (s - 1u - na) * 16u;
       const uint4 Pu = ld16(src + off);
       const v4u32 P = {Pu.x, Pu.y, Pu.z, Pu.w};
@@ -504,7 +584,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 // footprint (64 KiB tables + 8 KiB per wave) is what limits residency. One launch per AES round
 // count (a kernel holds only that count's round keys); the waves take the records of that round
 // count's work list (plan.hip, longest first) round-robin.
-template <bool OPEN, int kWaves, int NR, bool KS = false>
+template <bool OPEN, int kWaves, int NR, bool KS = false, bool BS = false>
 __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
@@ -537,7 +617,7 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
         continue;
       }
     }
-    gcm_record<NR, OPEN, KS>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
+    gcm_record<NR, OPEN, KS, BS>(A, d, A.ks + d.key_slot, r, lb, wb, lane, (uint32_t)(wave >> 2) % 3u);
     wave_lds_sync();  // table reads of this record done before the next record rebuilds it
   }
 }
@@ -552,8 +632,14 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
                                uint32_t* err, uint32_t n_slots, int nr_mask, int grid, hipStream_t s) {
   if (n == 0) return 0;
+  // ATLS_GCM_BS: fast steps per record done by bitsliced (VALU) steps instead of T-table (LDS)
+  // steps; 0 = the T-table-only kernel.
+  static const uint32_t bs_max = [] {
+    const char* v = getenv("ATLS_GCM_BS");
+    return v ? (uint32_t)atoi(v) : 0u;
+  }();
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, idx,
-                  (atls::PlanHdr*)plan, err, n_slots};
+                  (atls::PlanHdr*)plan, err, n_slots, nullptr, nullptr, bs_max};
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;
@@ -564,9 +650,14 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
   const dim3 block(64 * waves);
   const size_t lds = atls::lds_bytes(waves);
-#define ATLS_LAUNCH_NR(W, NR)                                                                  \
-  if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR>), dim3(g), block, lds, s, A);    \
-  else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR>), dim3(g), block, lds, s, A);
+#define ATLS_LAUNCH_NR(W, NR)                                                                              \
+  if (bs_max) {                                                                                            \
+    if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR, false, true>), dim3(g), block, lds, s, A);  \
+    else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR, false, true>), dim3(g), block, lds, s, A);      \
+  } else {                                                                                                 \
+    if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR>), dim3(g), block, lds, s, A);               \
+    else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR>), dim3(g), block, lds, s, A);                   \
+  }
 #define ATLS_LAUNCH(W)                                 \
   if (waves == W) {                                    \
     if (nr_mask & 1) { ATLS_LAUNCH_NR(W, 10) }         \
@@ -590,7 +681,7 @@ extern "C" int atls_launch_gcm_ks(int open, const void* ks, const atls_rec* recs
                                   uint32_t* err, uint32_t n_slots, int nr_mask, int grid, hipStream_t s) {
   if (n == 0) return 0;
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, nullptr, nullptr,
-                  err, n_slots, ksb, ks_ok};
+                  err, n_slots, ksb, ks_ok, 0u};
   constexpr int W = 12;
   const uint32_t want = (n + W - 1) / W;
   const uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;

@@ -210,6 +210,7 @@ struct GcmArgs {
   uint32_t n_slots;        // direct mode: key-table size
   const uint8_t* ksb;      // KS launches: keystream of ks_bs.hip, kKsStride blocks per record
   const uint8_t* ks_ok;    // KS launches: per record, 1 = keystream present (else T-tables)
+  uint32_t bs_max;         // BS kernels: fast steps per record done bitsliced (gcm.hip bs_steps)
 };
 
 // Open result for one record (record.rs:203-240 decrypt + padding scan). lastnz = (position <<
