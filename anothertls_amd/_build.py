@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libatls.so")
-SOURCES = ["engine.cpp", "keysetup.hip", "plan.hip", "gcm.hip", "chacha.hip", "hkdf.hip", "aes_block.hip", "ks_bs.hip", "stream.cpp"]
+SOURCES = ["engine.cpp", "keysetup.hip", "plan.hip", "gcm.hip", "chacha.hip", "hkdf.hip", "aes_block.hip", "stream.cpp"]
 ARCH = os.environ.get("ATLS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -14,7 +14,9 @@ def _stale():
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC)] + [os.path.join(HERE, "..", "include", "atls.h")]
+    # sources only: variant builds write objects under csrc/_obj, which must not make this look stale
+    deps = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".h"))]
+    deps.append(os.path.join(HERE, "..", "include", "atls.h"))
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 

@@ -16,7 +16,7 @@
 
 namespace atls {
 
-// Per key slot device state, built by the key-setup kernel (keysetup.hip). 4032 B, 16-B aligned.
+// Per key slot device state, built by the key-setup kernel (keysetup.hip). 2112 B, 16-B aligned.
 struct alignas(16) KeySched {
   uint32_t suite, nr, key_len, valid;  // nr = AES rounds (10/12/14), 0 for ChaCha
   uint32_t rk[60];                     // AES round keys as raw words (cipher.rs:216-249 expanded_key)
@@ -27,9 +27,8 @@ struct alignas(16) KeySched {
   uint32_t p4_be[32][4];               // x^(4p) * H^64, p = 0..31: seeds of the 4-bit GHASH tables
   uint32_t rkr[60];                    // rotl16(rk[i]): the T-table rounds' key words (gcm.hip)
   uint32_t pad[4];
-  uint32_t bsm[15][32];                // round-key bit masks of the bitsliced rounds (aes_bs.h make_masks)
 };
-static_assert(sizeof(KeySched) == 4032, "KeySched must be 4032 B");
+static_assert(sizeof(KeySched) == 2112, "KeySched must be 2112 B");
 
 constexpr int kSuiteAes128 = 0x1301, kSuiteAes256 = 0x1302, kSuiteChacha = 0x1303;
 

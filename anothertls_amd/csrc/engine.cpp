@@ -23,12 +23,6 @@
 #include "plan.h"
 
 extern "C" int atls_launch_build_t0(uint32_t* t0, hipStream_t s);
-extern "C" int atls_launch_ks(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* aux,
-                              uint8_t* out, uint8_t* ok, uint32_t n_slots, int nr_mask, int grid_wgs, hipStream_t s);
-extern "C" int atls_launch_gcm_ks(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
-                                  const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
-                                  atls_open_result* res, const uint32_t* t0, const uint8_t* ksb, const uint8_t* ks_ok,
-                                  uint32_t* err, uint32_t n_slots, int nr_mask, int grid, hipStream_t s);
 extern "C" int atls_launch_aes_blocks(int decrypt, const void* ks, const uint8_t* in, uint8_t* out, uint64_t nblocks,
                                       uint32_t* err, int grid, hipStream_t s);
 extern "C" int atls_launch_key_setup(const atls_key* keys, uint32_t n, void* ks, hipStream_t s);
@@ -84,10 +78,6 @@ struct atls_engine {
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
   DevBuf plan, plan_keys, plan_idx, plan_wg; // batch plan (plan.hip)
   DevBuf wgmax;                              // batch_prep: per-workgroup longest record
-  DevBuf ksbuf, ksok;                        // hybrid batches: keystream of ks_bs.hip
-  float hybrid_f = 0.0f;                     // ATLS_HYBRID: share of a direct AES batch keyed on the VALU
-  uint32_t hybrid_min = 8192;                // ATLS_HYBRID_MIN: smallest batch that splits
-  int hybrid_wgs = 2;                        // ATLS_HYBRID_WGS: keystream workgroups per CU
   int chacha_wgs = 8;                        // ATLS_CHACHA_WGS: ChaCha20-Poly1305 workgroups per CU
   bool force_plan = false;                   // ATLS_FORCE_PLAN=1: plan every batch (tests)
   bool no_pipeline = false;                  // ATLS_NO_PIPELINE=1: stage host batches in one piece
@@ -329,29 +319,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     if (rc) return rc;
     if (side && hipEventRecord(e->ev_side, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
-  // Hybrid direct AES batch: records [0, nb) get their AES-CTR keystream from the bitsliced
-  // kernel (VALU) on the second stream while the T-table kernel (LDS) seals [nb, n); then the KS
-  // launch seals [0, nb) from the keystream (ks_bs.hip).
-  const uint32_t nb = (!planned && e->has_aes && !side && e->hybrid_f > 0.0f && n >= e->hybrid_min)
-                          ? (uint32_t)((double)n * e->hybrid_f) : 0u;
-  if (nb) {
-    const size_t ks_bytes = (size_t)nb * atls::kKsStride * 16;
-    if (!e->ksbuf.reserve(ks_bytes + 16) || !e->ksok.reserve(nb)) return ATLS_INTERNAL_ERROR;
-    if (hipEventRecord(e->ev_plan, s) != hipSuccess || hipStreamWaitEvent(e->stream2, e->ev_plan, 0) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
-    rc = atls_launch_ks(open, e->ks.p, d_recs, nb, d_aux, (uint8_t*)e->ksbuf.p, (uint8_t*)e->ksok.p, e->n_slots,
-                        e->aes_nr_mask, e->cus * e->hybrid_wgs, e->stream2);
-    if (rc || hipEventRecord(e->ev_side, e->stream2) != hipSuccess) return rc ? rc : ATLS_INTERNAL_ERROR;
-    rc = atls_launch_gcm(open, e->ks.p, d_recs + nb, n - nb, d_in, d_aux, d_out,
-                         d_tags_out ? d_tags_out + 16 * (size_t)nb : nullptr,
-                         d_tags_in ? d_tags_in + 16 * (size_t)nb : nullptr, d_res ? d_res + nb : nullptr,
-                         (const uint32_t*)e->t0.p, nullptr, e->plan.p, (uint32_t*)e->err.p, e->n_slots,
-                         e->aes_nr_mask, e->cus, s);
-    if (rc || hipStreamWaitEvent(s, e->ev_side, 0) != hipSuccess) return rc ? rc : ATLS_INTERNAL_ERROR;
-    rc = atls_launch_gcm_ks(open, e->ks.p, d_recs, nb, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
-                            (const uint32_t*)e->t0.p, (const uint8_t*)e->ksbuf.p, (const uint8_t*)e->ksok.p,
-                            (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask, e->cus, s);
-  } else if (e->has_aes) {
+  if (e->has_aes) {
     rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, idx, e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask,
                          e->cus, s);
@@ -484,9 +452,6 @@ atls_engine* atls_engine_create(int device) {
   e->cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
   if (const char* v = std::getenv("ATLS_FORCE_PLAN")) e->force_plan = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_NO_PIPELINE")) e->no_pipeline = std::atoi(v) != 0;
-  if (const char* v = std::getenv("ATLS_HYBRID")) e->hybrid_f = std::min(0.9f, std::max(0.0f, (float)std::atof(v)));
-  if (const char* v = std::getenv("ATLS_HYBRID_MIN")) e->hybrid_min = (uint32_t)std::atoi(v);
-  if (const char* v = std::getenv("ATLS_HYBRID_WGS")) e->hybrid_wgs = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("ATLS_CHACHA_WGS")) e->chacha_wgs = std::max(1, std::atoi(v));
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
       hipStreamSynchronize(e->stream) != hipSuccess) {
@@ -501,7 +466,7 @@ void atls_engine_destroy(atls_engine* e) {
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
-  for (DevBuf* b : {&e->ksbuf, &e->ksok, &e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
+  for (DevBuf* b : {&e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
                     &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx, &e->plan_wg, &e->wgmax})
     b->release();
   if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);

@@ -22,7 +22,6 @@
 #include <cstdlib>
 
 #include "gcm_common.h"
-#include "aes_bs.h"
 
 namespace atls {
 
@@ -168,68 +167,6 @@ __device__ __forceinline__ void aes_ctr_r12(uint32_t (&s)[4], uint32_t addr1, co
 }
 #undef TA
 
-// ---- bitsliced steps (VALU) -------------------------------------------------------------------
-// The T-table rounds above are bound by the LDS (one ds_read_b32 per state byte and round) while
-// the VALU is about half idle. A bitsliced step does the AES of up to 8 consecutive fast steps of a
-// record at once with logic only (aes_bs.h: 8 counter blocks per lane, the blocks of slots
-// s, s + 64, ..., s + 448, so every load and store stays a coalesced 1 KiB run per wave); the XOR,
-// store and GHASH of each of those steps follow as in a fast step. Every wave mixes the two kinds
-// of steps within each record, so a CU always has LDS-bound and VALU-bound waves side by side.
-// Round keys come as bit masks from the key schedule (KeySched::bsm): wave-uniform scalar loads.
-template <int NR, bool OPEN>
-__device__ __forceinline__ void bs_steps(uint32_t base, uint32_t k, uint32_t na, const uint32_t (&nraw)[3], uint32_t ctr0,
-                                         const KeySched* ks, const uint8_t* src, uint8_t* dst, uint32_t (&y)[4],
-                                         int64_t& lastnz, bool tls, uint32_t wb, int lane) {
-  // data of this lane's k slots base + lane + 64 i: issued first, they land under the AES rounds
-  uint4 P[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++)
-    if ((uint32_t)i < k) P[i] = ld16(src + (base + 64u * i + (uint32_t)lane - 1u - na) * 16u);
-  // x[8c + b] = raw word c of the counter block of slot base + lane + 64 b (counter ctr0 + 64 b)
-  uint32_t x[32];
-#pragma unroll
-  for (int b = 0; b < 8; b++) {
-    x[b] = nraw[0];
-    x[8 + b] = nraw[1];
-    x[16 + b] = nraw[2];
-    x[24 + b] = bswap32(ctr0 + 64u * (uint32_t)b);
-  }
-  atls_bs::StateG<1> st;
-  atls_bs::blocks_to_group(x, st[0]);
-  const auto* bsm = cptr(&ks->bsm[0][0]);
-  {
-    atls_bs::Masks m;
-#pragma unroll
-    for (int q = 0; q < 32; q++) m[q >> 3][q & 7] = bsm[q];
-    atls_bs::add_round_key<1>(st, m);
-  }
-#pragma unroll 1
-  for (int rd = 1; rd <= NR; rd++) {
-    atls_bs::sub_bytes<1>(st);
-    atls_bs::Masks m;
-#pragma unroll
-    for (int q = 0; q < 32; q++) m[q >> 3][q & 7] = bsm[32 * rd + q];
-    if (rd < NR) atls_bs::shift_mix_ark<1>(st, m);
-    else atls_bs::shift_ark<1>(st, m);
-  }
-  atls_bs::group_to_blocks(st[0], x);
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    if ((uint32_t)i >= k) break;
-    const uint32_t off = (base + 64u * i + (uint32_t)lane - 1u - na) * 16u;
-    const v4u32 C = {P[i].x ^ x[i], P[i].y ^ x[8 + i], P[i].z ^ x[16 + i], P[i].w ^ x[24 + i]};
-    st16(dst + off, make_uint4(C.x, C.y, C.z, C.w));
-    if (OPEN && tls) {
-      const uint32_t cw[4] = {C.x, C.y, C.z, C.w};
-      const int j = last_nonzero(cw, 16);
-      if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((cw[j >> 2] >> (8 * (j & 3))) & 0xffu);
-    }
-    ghash_mul<ATLS_GHASH_W>(y, wb);
-    if (OPEN) { y[0] ^= P[i].x; y[1] ^= P[i].y; y[2] ^= P[i].z; y[3] ^= P[i].w; }
-    else { y[0] ^= C.x; y[1] ^= C.y; y[2] ^= C.z; y[3] ^= C.w; }
-  }
-}
-
 // Phase timing (build with -DATLS_TT_STAMPS): shader-clock totals over all records, read back with
 // atls_debug_tt_stamps(). 0 setup (tables, counter cache), 1 fast steps, 2 general steps,
 // 3 lane combine + tag, 4 records, 5 fast steps, 6 general steps.
@@ -240,9 +177,9 @@ __device__ unsigned long long g_tt_stamps[8];
 #define TT_STAMP(var)
 #endif
 
-template <int NR, bool OPEN, bool KS, bool BS>
+template <int NR, bool OPEN>
 __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx,
-                           uint32_t lb, uint32_t wb, int lane, uint32_t phase) {
+                           uint32_t lb, uint32_t wb, int lane) {
   TT_STAMP(t_start);
 #ifdef ATLS_TT_STAMPS
   uint64_t t_fast = 0, t_gen = 0, n_fast = 0, n_gen = 0;
@@ -343,10 +280,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   // Counter cache (CtrCache): every 64-slot step's counters share ctr >> 8 when the counter of slot
   // `base` is a multiple of 64 -- records with one AAD block (all TLS records) and a 96-bit IV.
   // Lane j holds the words of hi = j, enough for records below 2^14 blocks (256 KiB).
-  // KS launch: this record's counter blocks were encrypted by ks_bs.hip (bitsliced, on the VALU)
-  const bool use_ks = KS && A.ks_ok[rec_idx];
-  const uint8_t* kp = KS ? A.ksb + 16ull * kKsStride * rec_idx : nullptr;
-  const bool use_cache = ATLS_CTR_CACHE && is96 && na == 1u && S <= 64u * 256u && !use_ks;
+  const bool use_cache = ATLS_CTR_CACHE && is96 && na == 1u && S <= 64u * 256u;
   const uint32_t nraw[3] = {bswap32(j0[0]), bswap32(j0[1]), bswap32(j0[2])};
   const uint32_t lane_addr = ((uint32_t)lane << 8) | lb;  // T0 address of byte value `lane`
   const uint32_t k15 = rk[3] >> 24;                       // rk0 byte 15
@@ -370,36 +304,16 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   else if ((uint32_t)lane <= m) s_last = (int64_t)lane + (int64_t)((m - (uint32_t)lane) / 64) * 64;
   const uint32_t e_comb = s_last >= 1 ? S - (uint32_t)s_last : 1u;  // 1..64
 
-  // Bitsliced steps (BS kernels): up to A.bs_max of the record's F fast steps, as one window of
-  // consecutive steps whose place in the record depends on the wave (phase 0 / 1 / 2: first /
-  // middle / last), so that the waves of a SIMD are rarely in the same kind of step.
-  const uint32_t n_fast = fast_end >= 128u ? (fast_end - 64u) / 64u : 0u;
-  const uint32_t n_bs = (BS && is96 && !use_ks) ? min(A.bs_max, n_fast) : 0u;
-  const uint32_t bs_w0 = (n_fast - n_bs) * phase / 2u;
-
   TT_STAMP(t_setup);
   for (uint32_t base = 0; base < S; base += 64) {
     TT_STAMP(t_step);
     const uint32_t s = base + (uint32_t)lane;
     if (base >= 64u && base + 64u <= fast_end) {  // wave-uniform
-      if (BS && n_bs) {
-        const uint32_t fi = base / 64u - 1u;
-        if (fi >= bs_w0 && fi < bs_w0 + n_bs) {
-          const uint32_t kk = min(8u, bs_w0 + n_bs - fi);
-          bs_steps<NR, OPEN>(base, kk, na, nraw, j0[3] + base + (uint32_t)lane - na, k, src, dst, y, lastnz, tls, wb,
-                             lane);
-          base += 64u * (kk - 1u);
-          continue;
-        }
-      }
       const uint32_t off = (s - 1u - na) * 16u;
       const uint4 Pu = ld16(src + off);
       const v4u32 P = {Pu.x, Pu.y, Pu.z, Pu.w};
       uint32_t st[4];
-      if (use_ks) {
-        const uint4 kv = ld16(kp + 16u * (s - na));
-        st[0] = kv.x; st[1] = kv.y; st[2] = kv.z; st[3] = kv.w;
-      } else if (use_cache) {
+      if (use_cache) {
         const uint32_t c0 = j0[3] + base - na;  // counter of lane 0, a multiple of 64
         aes_cached(st, lane_addr ^ (((c0 & 0xffu) ^ k15) << 8), c0 >> 8);
       } else {
@@ -459,10 +373,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
         }
       }
     }
-    if (use_ks) {  // keystream block c (c = 0: E_K(J0)); lanes past the record read in-bounds junk
-      const uint4 kv = ld16(kp + 16u * min(c, kKsStride - 1u));
-      st[0] = kv.x; st[1] = kv.y; st[2] = kv.z; st[3] = kv.w;
-    } else if (use_cache) {  // ctr = 1 for slots 0..na, else 1 + s - na: the step's ctr >> 8 is lane 63's
+    if (use_cache) {  // ctr = 1 for slots 0..na, else 1 + s - na: the step's ctr >> 8 is lane 63's
       const uint32_t ctr = cb[3];
       const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)ctr, 63) >> 8;
       aes_cached(st, perm((ctr & 0xffu) ^ k15, lb, 0x0c0c0400u), hi);
@@ -584,7 +495,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 // footprint (64 KiB tables + 8 KiB per wave) is what limits residency. One launch per AES round
 // count (a kernel holds only that count's round keys); the waves take the records of that round
 // count's work list (plan.hip, longest first) round-robin.
-template <bool OPEN, int kWaves, int NR, bool KS = false, bool BS = false>
+template <bool OPEN, int kWaves, int NR>
 __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
@@ -617,7 +528,7 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
         continue;
       }
     }
-    gcm_record<NR, OPEN, KS, BS>(A, d, A.ks + d.key_slot, r, lb, wb, lane, (uint32_t)(wave >> 2) % 3u);
+    gcm_record<NR, OPEN>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
     wave_lds_sync();  // table reads of this record done before the next record rebuilds it
   }
 }
@@ -632,14 +543,8 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
                                uint32_t* err, uint32_t n_slots, int nr_mask, int grid, hipStream_t s) {
   if (n == 0) return 0;
-  // ATLS_GCM_BS: fast steps per record done by bitsliced (VALU) steps instead of T-table (LDS)
-  // steps; 0 = the T-table-only kernel.
-  static const uint32_t bs_max = [] {
-    const char* v = getenv("ATLS_GCM_BS");
-    return v ? (uint32_t)atoi(v) : 0u;
-  }();
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, idx,
-                  (atls::PlanHdr*)plan, err, n_slots, nullptr, nullptr, bs_max};
+                  (atls::PlanHdr*)plan, err, n_slots};
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;
@@ -650,14 +555,9 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
   const dim3 block(64 * waves);
   const size_t lds = atls::lds_bytes(waves);
-#define ATLS_LAUNCH_NR(W, NR)                                                                              \
-  if (bs_max) {                                                                                            \
-    if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR, false, true>), dim3(g), block, lds, s, A);  \
-    else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR, false, true>), dim3(g), block, lds, s, A);      \
-  } else {                                                                                                 \
-    if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR>), dim3(g), block, lds, s, A);               \
-    else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR>), dim3(g), block, lds, s, A);                   \
-  }
+#define ATLS_LAUNCH_NR(W, NR)                                                                  \
+  if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR>), dim3(g), block, lds, s, A);    \
+  else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR>), dim3(g), block, lds, s, A);
 #define ATLS_LAUNCH(W)                                 \
   if (waves == W) {                                    \
     if (nr_mask & 1) { ATLS_LAUNCH_NR(W, 10) }         \
@@ -673,29 +573,19 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
 
-// The KS launch of a hybrid batch (engine.cpp): records [0, n) of a direct batch whose keystream
-// atls_launch_ks wrote to ksb (ok per record in ks_ok; records without it use the T-tables).
-extern "C" int atls_launch_gcm_ks(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
-                                  const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
-                                  atls_open_result* res, const uint32_t* t0, const uint8_t* ksb, const uint8_t* ks_ok,
-                                  uint32_t* err, uint32_t n_slots, int nr_mask, int grid, hipStream_t s) {
-  if (n == 0) return 0;
-  atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, nullptr, nullptr,
-                  err, n_slots, ksb, ks_ok, 0u};
-  constexpr int W = 12;
-  const uint32_t want = (n + W - 1) / W;
-  const uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
-  const dim3 block(64 * W);
-  const size_t lds = atls::lds_bytes(W);
-#define ATLS_LAUNCH_NR(NR)                                                                          \
-  if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR, true>), dim3(g), block, lds, s, A);   \
-  else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR, true>), dim3(g), block, lds, s, A);
-  if (nr_mask == 1) { ATLS_LAUNCH_NR(10) }
-  else if (nr_mask == 2) { ATLS_LAUNCH_NR(12) }
-  else if (nr_mask == 4) { ATLS_LAUNCH_NR(14) }
-  else return ATLS_INTERNAL_ERROR;
-#undef ATLS_LAUNCH_NR
-  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+// Compile-time experiment switches this library was built with (include/atls.h
+// atls_build_flags): 0 for the product build, which must compute the reference's results.
+extern "C" unsigned atls_build_flags(void) {
+  unsigned f = 0;
+  if (ATLS_DBG_SKIP) f |= ATLS_BUILD_DBG_SKIP;
+  if (ATLS_DBG_SHARED_GHASH) f |= ATLS_BUILD_DBG_SHARED_GHASH;
+  if (ATLS_GHASH_W) f |= ATLS_BUILD_GHASH_W;
+  if (!ATLS_CTR_CACHE) f |= ATLS_BUILD_NO_CTR_CACHE;
+  if (ATLS_GHASH_ROT) f |= ATLS_BUILD_GHASH_ROT;
+#ifdef ATLS_TT_STAMPS
+  f |= ATLS_BUILD_TT_STAMPS;
+#endif
+  return f;
 }
 
 // Debug: copy out (and reset) the phase timers of a -DATLS_TT_STAMPS build; -1 otherwise.

@@ -1,7 +1,5 @@
-// Pieces shared by the two AES-GCM record kernels (gcm.hip: T-table AES, one record per wave;
-// gcm_bs.hip: bitsliced AES, two records per wave): LDS/VALU helpers, the 4-bit GHASH tables,
-// byte helpers for partial blocks, the kernel argument block, and the rule that splits a
-// batch between the two kernels.
+// Pieces of the AES-GCM record kernel (gcm.hip): LDS/VALU helpers, the 4-bit GHASH tables, the
+// comb multiply of the lane combine, byte helpers for partial blocks and the kernel argument block.
 #pragma once
 #include "plan.h"
 
@@ -208,9 +206,6 @@ struct GcmArgs {
   PlanHdr* plan;
   uint32_t* err;           // direct mode: sticky error word
   uint32_t n_slots;        // direct mode: key-table size
-  const uint8_t* ksb;      // KS launches: keystream of ks_bs.hip, kKsStride blocks per record
-  const uint8_t* ks_ok;    // KS launches: per record, 1 = keystream present (else T-tables)
-  uint32_t bs_max;         // BS kernels: fast steps per record done bitsliced (gcm.hip bs_steps)
 };
 
 // Open result for one record (record.rs:203-240 decrypt + padding scan). lastnz = (position <<

@@ -8,7 +8,6 @@
 // Also builds the 256-entry AES T-table T0 used (replicated per LDS bank) by gcm.hip.
 #include "aes_sbox.h"
 #include "atls_dev.h"
-#include "aes_bs.h"
 
 namespace atls {
 
@@ -87,13 +86,6 @@ __global__ void key_setup_kernel(const atls_key* __restrict__ keys, uint32_t n, 
                                    ((uint32_t)ek[4 * w + 2] << 16) | ((uint32_t)ek[4 * w + 3] << 24))
                                 : 0u;
   for (int w = 0; w < 60; w++) o->rkr[w] = (o->rk[w] << 16) | (o->rk[w] >> 16);
-  // bit masks of every round key for the bitsliced rounds (gcm.hip bitsliced steps)
-  for (int r = 0; r <= nr; r++) {
-    const uint32_t w[4] = {o->rk[4 * r], o->rk[4 * r + 1], o->rk[4 * r + 2], o->rk[4 * r + 3]};
-    atls_bs::Masks m;
-    atls_bs::make_masks(w, m);
-    for (int q = 0; q < 32; q++) o->bsm[r][q] = m[q >> 3][q & 7];
-  }
   o->nr = (uint32_t)nr;
   // H = E_K(0) (gcm.rs:56) and its powers.
   uint8_t zero[16] = {0}, hb[16];

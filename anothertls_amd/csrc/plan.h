@@ -10,9 +10,6 @@ constexpr int kPlanClasses = 16;  // length classes min(len >> 10, 15), longest 
 constexpr uint32_t kPlanReject = 0xffu;
 constexpr uint32_t kPlanKeys = kPlanLists * kPlanClasses;  // work-list keys (list, length class)
 constexpr uint32_t kPlanMaxWG = 1024;                      // plan workgroups (2 per CU)
-// Keystream buffer of ks_bs.hip: kKsStride 16-byte blocks per record (counters 0 .. nb + 1).
-constexpr uint32_t kKsUnits = 132;           // 8-counter units per record
-constexpr uint32_t kKsStride = 8 * kKsUnits;  // AEAD <= 16,848 B
 
 struct PlanHdr {
   uint32_t off[kPlanLists + 1];                  // list l = idx[off[l] .. off[l+1])

@@ -193,6 +193,13 @@ int atls_sb_read(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size
 /* Library info: ABI version and the device arch the code objects were built for ("gfx950"). */
 int atls_abi_version(void);
 const char* atls_device_arch(void);
+/* Compile-time experiment switches of this build (bit set, 0 for a product build). Timing
+ * experiments that drop work (ATLS_DBG_*) give wrong results; tests assert this is 0. */
+enum {
+  ATLS_BUILD_DBG_SKIP = 1u, ATLS_BUILD_DBG_SHARED_GHASH = 2u, ATLS_BUILD_GHASH_W = 4u,
+  ATLS_BUILD_NO_CTR_CACHE = 8u, ATLS_BUILD_GHASH_ROT = 16u, ATLS_BUILD_TT_STAMPS = 32u
+};
+unsigned atls_build_flags(void);
 
 #ifdef __cplusplus
 }

@@ -26,6 +26,14 @@ def test_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_product_build_has_no_experiment_switches():
+    """The library the package loads is the product build: no ATLS_DBG_* timing switch (those
+    drop work and give wrong results), no alternative GHASH / counter-cache variant."""
+    lib = atls.library()
+    lib.atls_build_flags.restype = __import__("ctypes").c_uint
+    assert lib.atls_build_flags() == 0
+
+
 def test_abi_version_and_arch():
     assert atls.abi_version() == 1
     assert atls.library().atls_device_arch() == b"gfx950"

@@ -1,4 +1,4 @@
-"""CPU check of the bitsliced AES core (anothertls_amd/csrc/aes_bs.h, the keystream kernel ks_bs.hip runs it) as it would run
+"""CPU check of the bitsliced AES core (tools/bitsliced/aes_bs.h, the bitsliced AES of the round-1/2 hybrid experiments) as it would run
 on the VALU: compiled for the host with software v_bitop3_b32 / v_perm_b32, 32 random blocks
 per key for AES-128/192/256 round keys from the oracle's key expansion, in the row-plane layout, compared against the
 oracle (literal restatement of crypto/aes/cipher.rs) block by block."""
@@ -88,7 +88,7 @@ def test_bitsliced_aes_matches_oracle():
         c = os.path.join(d, "t.cpp")
         exe = os.path.join(d, "t")
         open(c, "w").write(SRC)
-        subprocess.check_call(["g++", "-O1", "-I", os.path.join(ROOT, "anothertls_amd", "csrc"), c, "-o", exe])
+        subprocess.check_call(["g++", "-O1", "-I", os.path.join(ROOT, "tools", "bitsliced"), c, "-o", exe])
         rng = random.Random(99)
         for klen in (16, 24, 32):
             for _ in range(2):

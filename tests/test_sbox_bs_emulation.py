@@ -1,4 +1,4 @@
-"""CPU check of the generated bitsliced S-box (anothertls_amd/csrc/sbox_bs.h): compile it for the
+"""CPU check of the generated bitsliced S-box (tools/bitsliced/sbox_bs.h): compile it for the
 host with a software v_bitop3_b32 (result bit = tt[(a<<2)|(b<<1)|c], the gfx950 operand order
 observed in hipcc's own lowering) and compare all 256 inputs with the FIPS-197 S-box."""
 import os
@@ -49,6 +49,6 @@ def test_generated_sbox_matches_fips197():
         c = os.path.join(d, "t.cpp")
         exe = os.path.join(d, "t")
         open(c, "w").write(SRC)
-        subprocess.check_call(["g++", "-O1", "-I", os.path.join(ROOT, "anothertls_amd", "csrc"), c, "-o", exe])
+        subprocess.check_call(["g++", "-O1", "-I", os.path.join(ROOT, "tools", "bitsliced"), c, "-o", exe])
         out = subprocess.check_output([exe]).decode().strip()
     assert out == SBOX_HEX

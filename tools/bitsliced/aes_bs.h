@@ -1,6 +1,7 @@
-// Bitsliced AES for gfx950: 8 G blocks per lane, AES rounds as v_bitop3_b32 / v_perm_b32 /
-// v_alignbit_b32 logic on the VALU (no table lookups). Used by the keystream kernel
-// (ks_bs.hip), which runs on the VALU beside the LDS-bound T-table kernel (gcm.hip).
+// Bitsliced AES for gfx950 (tools only: the microbenchmarks and the CPU emulation tests; the product
+// kernel is T-table AES): 8 G blocks per lane, AES rounds as v_bitop3_b32 / v_perm_b32 /
+// v_alignbit_b32 logic on the VALU (no table lookups). Measured slower than the T-table kernel both
+// as a separate keystream kernel (round 1) and as steps mixed into the record kernel (round 2).
 //
 // Row-plane layout: st[g][r][j], g = block group (blocks 8g..8g+7), r = state row, j = bit
 // significance 7 - j (j = 0 is the MSB, the S-box circuit's U0). Bit 8c + b of a word is bit

@@ -1,4 +1,4 @@
-"""Generate anothertls_amd/csrc/sbox_bs.h: the AES S-box as a bitsliced circuit mapped onto
+"""Generate tools/bitsliced/sbox_bs.h: the AES S-box as a bitsliced circuit mapped onto
 gfx950 3-input LUT instructions (v_bitop3_b32).
 
 Source circuit: Boyar & Peralta's 128-gate AES S-box (XOR/XNOR/AND), checked exhaustively
@@ -157,7 +157,7 @@ def main():
             env[n] = cone_eval(cone, n, env)
         assert sum(env[f"S{i}"] << (7 - i) for i in range(8)) == SBOX[x]
     body = emit(cone, nodes)
-    hdr = os.path.join(os.path.dirname(__file__), "..", "..", "anothertls_amd", "csrc", "sbox_bs.h")
+    hdr = os.path.join(os.path.dirname(__file__), "sbox_bs.h")
     with open(hdr, "w") as f:
         f.write("// GENERATED by tools/bitsliced/gen_sbox_bitop3.py -- do not edit.\n")
         f.write("// Bitsliced AES S-box (Boyar-Peralta 128-gate circuit, LUT3-mapped onto v_bitop3_b32:\n")

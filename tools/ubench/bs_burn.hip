@@ -2,7 +2,7 @@
 // memory traffic) callable from Python beside the engine (tools/corun_gcm.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include "../../anothertls_amd/csrc/sbox_bs.h"
+#include "../bitsliced/sbox_bs.h"
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) { return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96); }
 __device__ __forceinline__ uint32_t rotr(uint32_t w, int n) { return n ? __builtin_amdgcn_alignbit(w, w, n) : w; }

@@ -6,7 +6,7 @@
 #include <stdio.h>
 #include <stdint.h>
 #include "../../anothertls_amd/csrc/gcm_common.h"
-#include "../../anothertls_amd/csrc/sbox_bs.h"
+#include "../bitsliced/sbox_bs.h"
 
 using namespace atls;
 #define TA(w, sh) perm((w), lb, 0x0c0c0000u | ((4u + (sh) / 8u) << 8))
