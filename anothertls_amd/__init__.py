@@ -61,6 +61,16 @@ _lib.atls_aes_blocks.argtypes = [_c.c_void_p, _c.c_int, _c.c_uint32, _c.c_void_p
                                  _c.c_uint32]
 _lib.atls_aes_block.argtypes = [_c.c_int, _c.c_void_p, _c.c_size_t, _c.c_void_p, _c.c_void_p]
 _lib.atls_device_arch.restype = _c.c_char_p
+_lib.atls_multi_create.restype = _c.c_void_p
+_lib.atls_multi_create.argtypes = [_c.c_void_p, _c.c_int]
+_lib.atls_multi_destroy.argtypes = [_c.c_void_p]
+_lib.atls_multi_devices.argtypes = [_c.c_void_p]
+_lib.atls_multi_uses_rccl.argtypes = [_c.c_void_p]
+_lib.atls_multi_set_keys.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32]
+_lib.atls_multi_seal_batch.argtypes = _lib.atls_seal_batch.argtypes
+_lib.atls_multi_open_batch.argtypes = _lib.atls_open_batch.argtypes
+_lib.atls_partition.restype = None
+_lib.atls_partition.argtypes = [_c.c_void_p, _c.c_uint32, _c.c_int, _c.c_uint32, _c.c_void_p]
 
 
 class TlsError(Exception):
@@ -316,6 +326,67 @@ class Engine:
         self._after_torch(recs, inp, aux, tags, out, results)
         _check(_lib.atls_open_batch(self._e, _ptr(recs), n, _ptr(inp), _ptr(aux), _ptr(tags), _ptr(out),
                                     _ptr(results), flags))
+
+
+def partition(recs, parts, open_=False):
+    """atls_partition: record boundaries [first[p], first[p+1]) of `parts` contiguous ranges
+    balanced by cumulative bytes (read + written + 16-byte tag per record). Host-only."""
+    recs = np.ascontiguousarray(recs, dtype=REC_DTYPE)
+    first = np.zeros(parts + 1, np.uint32)
+    _lib.atls_partition(recs.ctypes.data, len(recs), int(bool(open_)), parts, first.ctypes.data)
+    return first
+
+
+class MultiEngine:
+    """Several HIP devices in one process (atls_multi_*): a batch is split by cumulative bytes
+    into one contiguous record range per device; device-resident buffers live on devices[0] and
+    the other ranges travel over RCCL (distinct devices) or device copies (repeated devices)."""
+
+    def __init__(self, devices):
+        self.devices = [int(d) for d in devices]
+        arr = (_c.c_int * len(self.devices))(*self.devices)
+        self._m = _lib.atls_multi_create(arr, len(self.devices))
+        if not self._m:
+            raise TlsError(TlsError.INTERNAL_ERROR)
+
+    @property
+    def uses_rccl(self):
+        return bool(_lib.atls_multi_uses_rccl(self._m))
+
+    def close(self):
+        if self._m:
+            _lib.atls_multi_destroy(self._m)
+            self._m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_keys(self, keys):
+        keys = np.ascontiguousarray(keys, dtype=KEY_DTYPE)
+        _check(_lib.atls_multi_set_keys(self._m, keys.ctypes.data, len(keys)))
+
+    def _after_torch(self, *xs):
+        for x in xs:
+            if getattr(x, "is_cuda", False):
+                import torch
+
+                torch.cuda.synchronize(x.device)
+                return
+
+    def seal_batch(self, recs, inp, aux, out, tags, flags=0):
+        recs = np.ascontiguousarray(recs, dtype=REC_DTYPE)
+        self._after_torch(inp, aux, out, tags)
+        _check(_lib.atls_multi_seal_batch(self._m, recs.ctypes.data, len(recs), _ptr(inp), _ptr(aux), _ptr(out),
+                                          _ptr(tags), flags))
+
+    def open_batch(self, recs, inp, aux, tags, out, results, flags=0):
+        recs = np.ascontiguousarray(recs, dtype=REC_DTYPE)
+        self._after_torch(inp, aux, tags, out, results)
+        _check(_lib.atls_multi_open_batch(self._m, recs.ctypes.data, len(recs), _ptr(inp), _ptr(aux), _ptr(tags),
+                                          _ptr(out), _ptr(results), flags))
 
 
 def abi_version():

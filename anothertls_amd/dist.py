@@ -1,9 +1,11 @@
 """One process per GPU: rendezvous, sharding and whole-job timing for batch sealing.
 
 Records are independent, so a multi-GPU job is N copies of the single-GPU path over disjoint
-shards of the record stream (workload.shard_batch): no collective touches the data. The only
-collectives are the barriers around the timed region and one max-reduce of the wall time
-(torch.distributed; backend "nccl" = RCCL on ROCm between GPUs, "gloo" for CPU tests).
+shards of the record stream (workload.shard_batch): no collective touches the data of the timed
+path. Its only collectives are the barriers around the timed region and one max-reduce of the
+wall time (torch.distributed; backend "nccl" = RCCL on ROCm between GPUs, "gloo" for CPU tests).
+A batch that arrives at one rank is spread with seal_sharded: a byte-balanced split, RCCL
+point-to-point scatter of the record ranges, per-rank sealing and a gather back.
 """
 import os
 import time
@@ -23,8 +25,11 @@ def init(backend, device=None):
     if world <= 1:
         return False
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    import datetime
+
     kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
-    tdist.init_process_group(backend, **kw)
+    # every collective here takes seconds at most: fail instead of hanging a benchmark run
+    tdist.init_process_group(backend, timeout=datetime.timedelta(seconds=300), **kw)
     return True
 
 
@@ -64,38 +69,76 @@ def whole_job_rate(bytes_per_rank, steps, wall, world):
     return world * bytes_per_rank * steps / wall / 2**30
 
 
-def scatter_gather(nbytes, device=None, reps=3):
-    """Time the exchange the bulk path needs when a batch arrives at one rank:
-    rank 0 scatters `nbytes` of records to every rank and gathers `nbytes` of sealed output back
-    (torch.distributed scatter / gather: RCCL over xGMI for "nccl", gloo on CPU). Not on the
-    timed sealing path. Returns (scatter_GBps, gather_GBps) of the bytes leaving / entering rank
-    0 for the other ranks, max time over ranks, or None for a single rank."""
-    if not (tdist.is_available() and tdist.is_initialized()):
-        return None
-    rank, world = tdist.get_rank(), tdist.get_world_size()
-    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
-    parts = [torch.full((nbytes,), r, dtype=torch.uint8, device=device) for r in range(world)] if rank == 0 else None
+def extents(recs, open_=False):
+    """Per record: bytes read at in_off and written at out_off (include/atls.h modes: TLS seal
+    writes content + type byte, WIRE seal header || ct || tag, WIRE open reads the wire record)."""
+    import numpy as np
 
-    def sync():
-        if device is not None and device.type == "cuda":
-            torch.cuda.synchronize(device)
+    L = recs["len"].astype(np.int64)
+    mode = recs["mode"]
+    if open_:
+        return np.where(mode == 2, L + 21, L), L
+    return L, np.where(mode == 1, L, np.where(mode == 2, L + 22, L + 1))
 
-    def timed(fn):
-        fn()  # warm-up (communicator, buffers)
-        sync()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            fn()
-        sync()
-        return max_over_ranks((time.perf_counter() - t0) / reps, device)
 
-    ts = timed(lambda: tdist.scatter(buf, scatter_list=parts, src=0))
-    if not bool((buf == rank).all()):
-        raise RuntimeError("scatter delivered the wrong shard")
-    tg = timed(lambda: tdist.gather(buf, gather_list=parts, dst=0))
-    moved = (world - 1) * nbytes / 1e9
-    return moved / ts, moved / tg
+def seal_sharded(seal, recs, inp=None, out=None, tags=None, device=None):
+    """Seal one batch that arrives at rank 0 with every rank's GPU: the records are cut into
+    contiguous ranges balanced by cumulative bytes (atls_partition, the split the C ABI's
+    atls_multi_* uses), rank 0 sends each rank its range's input bytes (and its output range, so
+    bytes between records survive), every rank seals its range with `seal(recs, inp, out, tags)`
+    on rebased descriptors (rank 0 in place), and the sealed ranges and tags come back into
+    rank 0's `out` / `tags`. Point-to-point torch.distributed (RCCL over xGMI for "nccl", gloo
+    on CPU). `recs` (the numpy descriptors) on every rank; the tensors on rank 0 only. Ranges
+    must increase with the record index, as in atls_multi_*. Returns this rank's record range."""
+    import numpy as np
+
+    import anothertls_amd as atls
+
+    initialized = tdist.is_available() and tdist.is_initialized()
+    rank, world = (tdist.get_rank(), tdist.get_world_size()) if initialized else (0, 1)
+    first = atls.partition(recs, world)
+    ilen, olen = extents(recs)
+
+    def span(r):
+        a, b = int(first[r]), int(first[r + 1])
+        if a == b:
+            return a, b, 0, 0, 0, 0
+        return (a, b, int(recs["in_off"][a]), int(recs["in_off"][b - 1]) + int(ilen[b - 1]),
+                int(recs["out_off"][a]), int(recs["out_off"][b - 1]) + int(olen[b - 1]))
+
+    a, b, in_lo, in_hi, out_lo, out_hi = span(rank)
+    if rank == 0:
+        reqs = []
+        for r in range(1, world):
+            ra, rb, ilo, ihi, olo, ohi = span(r)
+            if ra < rb:
+                reqs += [tdist.isend(inp[ilo:ihi], dst=r), tdist.isend(out[olo:ohi], dst=r)]
+        if a < b:
+            seal(recs[a:b], inp, out, tags[16 * a:16 * b])
+        for q in reqs:
+            q.wait()
+        reqs = []
+        for r in range(1, world):
+            ra, rb, ilo, ihi, olo, ohi = span(r)
+            if ra < rb:
+                reqs += [tdist.irecv(out[olo:ohi], src=r), tdist.irecv(tags[16 * ra:16 * rb], src=r)]
+        for q in reqs:
+            q.wait()
+    elif a < b:
+        import torch
+
+        loc_in = torch.empty(in_hi - in_lo, dtype=torch.uint8, device=device)
+        loc_out = torch.empty(out_hi - out_lo, dtype=torch.uint8, device=device)
+        loc_tags = torch.empty(16 * (b - a), dtype=torch.uint8, device=device)
+        tdist.recv(loc_in, src=0)
+        tdist.recv(loc_out, src=0)
+        local = recs[a:b].copy()
+        local["in_off"] -= np.uint64(in_lo)
+        local["out_off"] -= np.uint64(out_lo)
+        seal(local, loc_in, loc_out, loc_tags)
+        tdist.send(loc_out, dst=0)
+        tdist.send(loc_tags, dst=0)
+    return a, b
 
 
 def close():

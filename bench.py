@@ -56,7 +56,8 @@ def parse():
     p.add_argument("--pcie", action="store_true", help="also time host-memory (PCIe-inclusive) batches")
     p.add_argument("--wire", action="store_true",
                    help="also time the same records sealed as one wire stream (ATLS_MODE_WIRE)")
-    p.add_argument("--no-scatter", action="store_true", help="N > 1: skip the RCCL scatter/gather timing")
+    p.add_argument("--no-scatter", action="store_true",
+                   help="N > 1: skip the sharded scatter / seal / gather of rank 0's batch")
     return p.parse_args()
 
 
@@ -94,6 +95,37 @@ def cpu_baseline(batch, inbuf_host, budget_s, threads):
                 sample=f"{dn} record seals ({pn} B AEAD payload) cycling over the first {n_rec} records of the same "
                        f"batch, oracle/ref_restatement.c ora_seal_batch, {threads} threads, {tn:.1f} s; 1 thread: "
                        f"{d1} records ({p1} B) in {t1:.1f} s")
+
+
+def sharded_exchange(args, eng, dev, d_in, d_aux, d_ref_out, d_ref_tags, reps=3):
+    """Rank 0's batch (its shard of the config) sealed by all ranks through dist.seal_sharded
+    (byte-balanced split, RCCL point-to-point scatter / gather, each rank's engine on its range).
+    Returns (rank 0) GiB/s of AEAD payload for scatter + seal + gather, max time over ranks, and
+    whether the gathered bytes equal rank 0's single-GPU result."""
+    import anothertls_amd as atls
+    from anothertls_amd import workload
+
+    b0 = workload.shard_batch(args.config, 0, n=args.records, n_keys=args.key_slots)  # same on every rank
+    rank = dist.env_ranks()[0]
+    out = tags = None
+    if rank == 0:
+        out = torch.zeros_like(d_ref_out)
+        tags = torch.zeros_like(d_ref_tags)
+
+    def seal(recs, inp, o, t):
+        eng.seal_batch(recs, inp, d_aux, o, t, flags=atls.FLAG_DEVICE_PTRS)  # synchronous
+
+    def run():
+        dist.seal_sharded(seal, b0["recs"], d_in, out, tags, device=dev)
+
+    run()  # warm-up: communicators, staging
+    wall = dist.timed_steps(run, reps, 0, lambda: torch.cuda.synchronize(dev), dev)
+    if rank != 0:
+        return None
+    match = bool(torch.equal(out, d_ref_out) and torch.equal(tags, d_ref_tags))
+    return {"GiBps": round(b0["payload"] * reps / wall / 2**30, 3), "ms": round(wall / reps * 1e3, 3),
+            "matches_single_gpu": match, "records": len(b0["recs"]),
+            "path": "dist.seal_sharded: atls_partition byte split, torch.distributed P2P (RCCL over xGMI)"}
 
 
 C1 = "c1_server_https_loopback_1MiB"
@@ -289,17 +321,18 @@ def main():
         sync()
         result["wire_GiBps"] = round(payload * args.steps / (w0.elapsed_time(w1) * 1e-3) / 2**30, 3)
     if world > 1 and not args.no_scatter:
-        # host-arrival exchange beside the sealing path: rank 0 scatters / gathers a
-        # 64 MiB shard per rank over RCCL; reported, not part of `value`
+        # A batch arriving at one GPU: rank 0's shard is split by cumulative bytes
+        # over all ranks, scattered over RCCL, sealed by every rank's engine and gathered back
+        # (dist.seal_sharded); reported beside `value`, which is the pre-sharded rate. The result
+        # must equal rank 0's own single-GPU seal of the same records (d_out / d_tags above).
         try:
-            sg = dist.scatter_gather(64 << 20, dev)
+            sg = sharded_exchange(args, eng, dev, d_in if rank == 0 else None, d_aux, d_out if rank == 0 else None,
+                                  d_tags if rank == 0 else None)
         except Exception as exc:  # the bench line must survive a collective failure
             sg = None
-            print(f"scatter/gather measurement failed: {exc}", file=sys.stderr, flush=True)
+            print(f"sharded exchange failed: {exc}", file=sys.stderr, flush=True)
         if rank == 0 and result is not None:
-            result["scatter_gather"] = None if sg is None else {
-                "scatter_GBps": round(sg[0], 1), "gather_GBps": round(sg[1], 1), "bytes_per_rank": 64 << 20,
-                "backend": "nccl (RCCL over xGMI)"}
+            result["sharded_from_rank0"] = sg
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -166,6 +166,32 @@ int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* 
 /* One block with a raw key (16/24/32 B) on the process-default engine. */
 int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_t in[16], uint8_t out[16]);
 
+/* ---- Multi-GPU batches (one process, several devices), SURVEY.md §8(b)/(e) ----------------
+ * Records are independent (the nonce is (static_iv, seq), key_schedule.rs:51-64), so a batch
+ * splits into contiguous record ranges balanced by cumulative bytes, one per device, each sealed
+ * or opened by that device's engine with rebased descriptors; outputs, tags and open results land
+ * in the caller's buffers exactly as one engine would write them.
+ * devices[0] is the root: with ATLS_FLAG_DEVICE_PTRS the buffers live on it and the other ranges
+ * are scattered / gathered over RCCL (grouped send/recv over xGMI) when all devices are distinct,
+ * or by device-to-device copies when the list repeats a device. Host buffers: every device stages
+ * its own range over its own link. Descriptors are host arrays whose in/out ranges increase with
+ * the record index (else ATLS_ILLEGAL_PARAMETER); ATLS_FLAG_DEVICE_RECS / ATLS_FLAG_NO_SYNC are not
+ * accepted. Key slots are installed on every device. */
+typedef struct atls_multi atls_multi;
+atls_multi* atls_multi_create(const int* devices, int n_devices); /* NULL if a device or RCCL fails */
+void atls_multi_destroy(atls_multi* m);
+int atls_multi_devices(const atls_multi* m);
+int atls_multi_uses_rccl(const atls_multi* m); /* 1: RCCL transport, 0: device copies / single device */
+int atls_multi_set_keys(atls_multi* m, const atls_key* keys, uint32_t n);
+int atls_multi_seal_batch(atls_multi* m, const atls_rec* recs, uint32_t n, const void* in, const void* aux, void* out,
+                          uint8_t* tags, uint32_t flags);
+int atls_multi_open_batch(atls_multi* m, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
+                          const uint8_t* tags, void* out, atls_open_result* results, uint32_t flags);
+/* The split both use: first[p] .. first[p+1]-1 are part p's records (first[parts] = n), cut where
+ * the cumulative cost (bytes read + bytes written + 16-byte tag per record) crosses p/parts of
+ * the total. Host-only, no device needed. */
+void atls_partition(const atls_rec* recs, uint32_t n, int open, uint32_t parts, uint32_t* first);
+
 /* ---- Batched record streams (TlsStream::tls_write / tls_read, net/stream.rs:32-150) -------
  * Many connections over one engine: atls_sb_write queues a connection's records (fragmented at
  * 2^14 bytes, RFC 8446 §5.1), atls_sb_flush seals the queued records of every connection in one

@@ -1,7 +1,9 @@
-"""Multi-rank path on CPU (world size 2, gloo): shards are disjoint slices of the config's record
-stream, the per-rank results of the sealing step (here the oracle, standing in for the GPU) put
-together equal the unsharded batch's, and the timing helpers (barriers + max over ranks)
-behave as bench.py relies on."""
+"""Multi-rank path on CPU (world size 2, gloo): a batch that arrives at rank 0 is split by
+cumulative bytes (atls_partition), scattered, sealed per rank and gathered back by
+dist.seal_sharded -- here with the oracle as each rank's sealer, so the exchange logic runs on CPU
+(tests/test_gpu_dist.py runs the same function with the real engine on the GPU box) -- and the
+result equals the unsharded batch byte for byte, gaps between records included. Also the timing
+helpers (barriers + max over ranks) bench.py relies on."""
 import os
 import socket
 import sys
@@ -11,7 +13,7 @@ import pytest
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-N_PER_RANK = 24
+N_RECORDS = 48
 CONFIG = "c5_mixed_256Ki_x_64B-16KiB"
 
 
@@ -21,17 +23,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _seal_shard(batch, seed):
+def _oracle_sealer(keys):
     import oracle as ora
-    from test_gpu_parity import oracle_keys, oracle_recs
 
-    rng = np.random.default_rng(seed)
-    inbuf = rng.integers(0, 256, size=batch["in_bytes"] + 16, dtype=np.uint8)
-    out = np.zeros(batch["out_bytes"] + 16, np.uint8)
-    tags = np.zeros(16 * len(batch["recs"]), np.uint8)
-    assert ora.seal_batch(oracle_keys(batch["keys"]), oracle_recs(batch["recs"]), inbuf, np.zeros(16, np.uint8),
-                          out, tags, 1) == 0
-    return inbuf, out, tags
+    okeys = (ora.OraKey * len(keys)).from_buffer_copy(keys.tobytes())
+
+    def seal(recs, inp, out, tags):
+        orecs = (ora.OraRec * len(recs)).from_buffer_copy(recs.tobytes())
+        assert ora.seal_batch(okeys, orecs, inp.numpy(), np.zeros(16, np.uint8), out.numpy(), tags.numpy(), 1) == 0
+
+    return seal
+
+
+def _payload(batch):
+    return np.random.default_rng(7).integers(0, 256, size=batch["in_bytes"] + 16, dtype=np.uint8)
 
 
 def _worker(rank, world, port, q):
@@ -39,28 +44,28 @@ def _worker(rank, world, port, q):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port), ATLS_NO_TORCH_RUNTIME="1")
-    import torch.distributed as tdist
+    import torch
 
     from anothertls_amd import dist, workload
 
     assert dist.init("gloo")
-    batch = workload.shard_batch(CONFIG, rank, n=N_PER_RANK)
-    inbuf, out, tags = _seal_shard(batch, 100 + rank)
+    batch = workload.config_batch(CONFIG, n=N_RECORDS)
+    inp = out = tags = None
+    if rank == 0:
+        inp = torch.from_numpy(_payload(batch))
+        out = torch.full((batch["out_bytes"] + 16,), 0xA5, dtype=torch.uint8)  # gap bytes must survive
+        tags = torch.zeros(16 * N_RECORDS, dtype=torch.uint8)
+    a, b = dist.seal_sharded(_oracle_sealer(batch["keys"]), batch["recs"], inp, out, tags)
     calls = []
     wall = dist.timed_steps(lambda: calls.append(1), steps=5, warmup=2, sync=lambda: None)
-    # rank 1 reports a longer time: the max must win on every rank
-    mx = dist.max_over_ranks(1.0 + rank)
-    # bench.py's scatter/gather timing (RCCL on the GPU box): shards arrive intact, rates > 0
-    sg = dist.scatter_gather(1 << 16)
-    assert sg is not None and sg[0] > 0 and sg[1] > 0
-    gathered = [None] * world
-    tdist.all_gather_object(gathered, (batch["recs"].tobytes(), inbuf.tobytes(), out.tobytes(), tags.tobytes()))
-    q.put((rank, len(calls), wall, mx, gathered if rank == 0 else None))
+    mx = dist.max_over_ranks(1.0 + rank)  # rank 1 reports a longer time: the max must win everywhere
+    q.put((rank, a, b, len(calls), wall, mx,
+           (out.numpy().tobytes(), tags.numpy().tobytes()) if rank == 0 else None))
     dist.close()
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_shards_match_unsharded_batch():
+def test_two_rank_sharded_seal_matches_unsharded_batch():
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -72,41 +77,42 @@ def test_two_rank_shards_match_unsharded_batch():
         p.join(60)
         assert p.exitcode == 0
     res.sort(key=lambda r: r[0])
-    for rank, ncalls, wall, mx, _ in res:
+    for rank, a, b, ncalls, wall, mx, _ in res:
         assert ncalls == 7 and wall >= 0.0 and mx == 2.0, (rank, ncalls, wall, mx)
-    gathered = res[0][4]
+    # the two ranges tile the batch and are balanced by bytes, not by count
+    assert res[0][1] == 0 and res[0][2] == res[1][1] and res[1][2] == N_RECORDS
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from anothertls_amd import REC_DTYPE, workload
+    import torch
 
-    full = workload.config_batch(CONFIG, n=world * N_PER_RANK)
-    recs = [np.frombuffer(g[0], REC_DTYPE) for g in gathered]
-    for f in ("len", "key_slot", "seq", "content_type", "mode"):
-        assert np.array_equal(np.concatenate([r[f] for r in recs]), full["recs"][f]), f
-    # the unsharded batch sealed with the shards' payloads gives the shards' tags and bytes
-    for rank, g in enumerate(gathered):
-        shard = workload.shard_batch(CONFIG, rank, n=N_PER_RANK)
-        inbuf = np.frombuffer(g[1], np.uint8)
-        _, out, tags = _seal_shard(shard, 100 + rank)
-        assert np.frombuffer(g[3], np.uint8).tobytes() == tags.tobytes()
-        assert np.frombuffer(g[2], np.uint8).tobytes() == out.tobytes()
-        # and each shard record equals the same record sealed inside the full batch
-        sub = dict(full)
-        lo = rank * N_PER_RANK
-        sub_recs = full["recs"][lo:lo + N_PER_RANK].copy()
-        sub_recs["in_off"] = shard["recs"]["in_off"]
-        sub_recs["out_off"] = shard["recs"]["out_off"]
-        sub = dict(keys=full["keys"], recs=sub_recs, in_bytes=shard["in_bytes"], out_bytes=shard["out_bytes"])
-        _, out2, tags2 = _seal_shard_with(sub, inbuf)
-        assert tags2.tobytes() == tags.tobytes() and out2.tobytes() == out.tobytes()
+    from anothertls_amd import workload
+
+    batch = workload.config_batch(CONFIG, n=N_RECORDS)
+    L = batch["recs"]["len"].astype(np.int64)
+    cut = res[0][2]
+    assert abs(int(L[:cut].sum()) - int(L[cut:].sum())) <= int(L.max()) + 64
+    out = torch.full((batch["out_bytes"] + 16,), 0xA5, dtype=torch.uint8)
+    tags = torch.zeros(16 * N_RECORDS, dtype=torch.uint8)
+    _oracle_sealer(batch["keys"])(batch["recs"], torch.from_numpy(_payload(batch)), out, tags)
+    got_out, got_tags = res[0][6]
+    assert got_tags == tags.numpy().tobytes()
+    assert got_out == out.numpy().tobytes()
 
 
-def _seal_shard_with(batch, inbuf):
-    import oracle as ora
-    from test_gpu_parity import oracle_keys, oracle_recs
+def test_partition_balances_cumulative_bytes():
+    import anothertls_amd as atls
+    from anothertls_amd import workload
 
-    out = np.zeros(batch["out_bytes"] + 16, np.uint8)
-    tags = np.zeros(16 * len(batch["recs"]), np.uint8)
-    assert ora.seal_batch(oracle_keys(batch["keys"]), oracle_recs(batch["recs"]), inbuf, np.zeros(16, np.uint8),
-                          out, tags, 1) == 0
-    return inbuf, out, tags
+    b = workload.config_batch(CONFIG, n=32768)
+    L = b["recs"]["len"].astype(np.int64) * 2 + 17
+    for parts in (1, 2, 3, 8):
+        first = atls.partition(b["recs"], parts)
+        assert first[0] == 0 and first[-1] == len(L) and (np.diff(first) >= 0).all()
+        share = np.array([L[first[i]:first[i + 1]].sum() for i in range(parts)])
+        assert share.max() - share.min() <= 2 * 16401, (parts, share)
+    # C4-like equal records: equal counts
+    c4 = workload.config_batch("c4_aes256gcm_1Mi_x_16KiB", n=8 * 1000)
+    assert (np.diff(atls.partition(c4["recs"], 8)) == 1000).all()
+    # more parts than records: empty parts, still a tiling
+    f = atls.partition(b["recs"][:3], 8)
+    assert f[0] == 0 and f[-1] == 3 and (np.diff(f) >= 0).all()

@@ -1,0 +1,152 @@
+"""Multi-GPU paths of the product on the GPU box (one GPU there, so several ranges share device 0):
+
+* atls_multi_* (MultiEngine): a batch split by cumulative bytes over several engines, scattered,
+  sealed / opened and gathered, equals one engine's result byte for byte (bytes between records
+  included), for device-resident and host buffers, TLS and WIRE records, and tampered-tag opens.
+  With a repeated device the transport is device-to-device copies; distinct GPUs use RCCL (the
+  same code path around it; not exercisable on a one-GPU box).
+* dist.seal_sharded with the real engine in two ranks (gloo, both on device 0): the batch at
+  rank 0 is scattered, each rank's engine seals its range, and the gathered result equals the
+  unsharded batch.
+Reference: records are independent because nonce = static_iv ^ seq (net/key_schedule.rs:51-64)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+import anothertls_amd as atls
+from anothertls_amd import workload
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _batch(n=3000):
+    b = workload.config_batch("c5_mixed_256Ki_x_64B-16KiB", n=n)
+    inbuf = np.random.default_rng(3).integers(0, 256, b["in_bytes"] + 16, dtype=np.uint8)
+    return b, inbuf
+
+
+def _single_seal(b, inbuf, recs=None, out_bytes=None):
+    recs = b["recs"] if recs is None else recs
+    e = atls.Engine(0)
+    e.set_keys(b["keys"])
+    out = np.full((out_bytes or b["out_bytes"]) + 16, 0x5A, np.uint8)
+    tags = np.zeros(16 * len(recs), np.uint8)
+    e.seal_batch(recs, inbuf, np.zeros(16, np.uint8), out, tags)
+    e.close()
+    return out, tags
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_engine_device_buffers_equal_single_engine(devices):
+    b, inbuf = _batch()
+    ref_out, ref_tags = _single_seal(b, inbuf)
+    m = atls.MultiEngine(devices)
+    assert not m.uses_rccl  # repeated / single device: copies
+    m.set_keys(b["keys"])
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(inbuf).to(dev)
+    d_out = torch.full((b["out_bytes"] + 16,), 0x5A, dtype=torch.uint8, device=dev)
+    d_tags = torch.zeros(16 * len(b["recs"]), dtype=torch.uint8, device=dev)
+    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+    m.seal_batch(b["recs"], d_in, d_aux, d_out, d_tags, flags=atls.FLAG_DEVICE_PTRS)
+    assert np.array_equal(d_tags.cpu().numpy(), ref_tags)
+    assert np.array_equal(d_out.cpu().numpy(), ref_out)
+    # open through the multi engine, with a few tampered tags
+    recs = b["recs"]
+    orecs = recs.copy()
+    orecs["in_off"] = recs["out_off"]
+    orecs["len"] = recs["len"] + 1
+    bad = [5, 1500, 2999]
+    d_tags[torch.tensor(bad) * 16] ^= 1
+    d_back = torch.zeros_like(d_out)
+    d_res = torch.zeros(8 * len(recs), dtype=torch.uint8, device=dev)
+    m.open_batch(orecs, d_out, d_aux, d_tags, d_back, d_res, flags=atls.FLAG_DEVICE_PTRS)
+    res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
+    mask = np.zeros(len(recs), bool)
+    mask[bad] = True
+    assert (res["status"][mask] == 50).all() and (res["status"][~mask] == 0).all()
+    assert (res["content_len"][~mask] == recs["len"][~mask]).all()
+    back = d_back.cpu().numpy()
+    for i in np.flatnonzero(~mask)[::97]:
+        o, s, L = int(recs[i]["out_off"]), int(recs[i]["in_off"]), int(recs[i]["len"])
+        assert back[o:o + L].tobytes() == inbuf[s:s + L].tobytes()
+    m.close()
+
+
+def test_multi_engine_host_buffers_and_wire_records():
+    b, inbuf = _batch(1200)
+    wb = workload.wire_batch(b)
+    ref_out, ref_tags = _single_seal(b, inbuf, wb["recs"], wb["out_bytes"])
+    m = atls.MultiEngine([0, 0, 0, 0])
+    m.set_keys(b["keys"])
+    out = np.full(wb["out_bytes"] + 16, 0x5A, np.uint8)
+    tags = np.zeros(16 * len(b["recs"]), np.uint8)
+    m.seal_batch(wb["recs"], inbuf, np.zeros(16, np.uint8), out, tags)  # host memory: each part stages its range
+    assert np.array_equal(tags, ref_tags) and np.array_equal(out, ref_out)
+    # interleaved ranges are refused (the split needs offsets increasing with the index)
+    r2 = b["recs"][::-1].copy()
+    with pytest.raises(atls.TlsError) as e:
+        m.seal_batch(r2, inbuf, np.zeros(16, np.uint8), out, tags)
+    assert e.value.code == 47
+    m.close()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(RANK=str(rank), LOCAL_RANK="0", WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import torch as t
+
+    import anothertls_amd as a
+    from anothertls_amd import dist
+
+    assert dist.init("gloo")
+    b, inbuf = _batch(2000)
+    eng = a.Engine(0)
+    eng.set_keys(b["keys"])
+
+    def seal(recs, inp, out, tags):  # host tensors (gloo): the engine stages them over PCIe
+        eng.seal_batch(recs, inp.numpy(), np.zeros(16, np.uint8), out.numpy(), tags.numpy())
+
+    inp = out = tags = None
+    if rank == 0:
+        inp = t.from_numpy(inbuf)
+        out = t.full((b["out_bytes"] + 16,), 0x5A, dtype=t.uint8)
+        tags = t.zeros(16 * len(b["recs"]), dtype=t.uint8)
+    rng = dist.seal_sharded(seal, b["recs"], inp, out, tags)
+    q.put((rank, rng, (out.numpy().tobytes(), tags.numpy().tobytes()) if rank == 0 else None))
+    eng.close()
+    dist.close()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_seal_sharded_with_engine():
+    import torch.multiprocessing as mp
+
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0][1][0] == 0 and res[0][1][1] == res[1][1][0] and res[1][1][1] == 2000
+    b, inbuf = _batch(2000)
+    ref_out, ref_tags = _single_seal(b, inbuf)
+    got_out, got_tags = res[0][2]
+    assert got_tags == ref_tags.tobytes()
+    assert got_out == ref_out.tobytes()
