@@ -52,6 +52,7 @@ _lib.atls_engine_sync.argtypes = [_c.c_void_p]
 _lib.atls_engine_stream.restype = _c.c_void_p
 _lib.atls_engine_stream.argtypes = [_c.c_void_p]
 _lib.atls_set_keys.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32]
+_lib.atls_update_keys.argtypes = [_c.c_void_p, _c.c_uint32, _c.c_void_p, _c.c_uint32]
 _lib.atls_seal_batch.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
                                  _c.c_void_p, _c.c_uint32]
 _lib.atls_open_batch.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_void_p, _c.c_void_p, _c.c_void_p,
@@ -288,6 +289,11 @@ class Engine:
     def set_keys(self, keys):
         keys = np.ascontiguousarray(keys, dtype=KEY_DTYPE)
         _check(_lib.atls_set_keys(self._e, keys.ctypes.data, len(keys)))
+
+    def update_keys(self, first, keys):
+        """Install key slots [first, first + len(keys)), keeping the other slots."""
+        keys = np.ascontiguousarray(keys, dtype=KEY_DTYPE)
+        _check(_lib.atls_update_keys(self._e, int(first), keys.ctypes.data, len(keys)))
 
     def derive_keys(self, suite, secrets):
         """Key::from_hkdf for each traffic secret (bytes-like, n * hash_len) -> KEY_DTYPE array."""

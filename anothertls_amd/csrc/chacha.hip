@@ -401,7 +401,7 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
   if (q >= cnt) return;
   const uint32_t r = W.record(q);
   const atls_rec d = A.recs[r];
-  const uint32_t st = A.idx ? 0u : direct_reject(d, A.ks, A.n_slots);  // direct mode
+  const uint32_t st = A.idx ? 0u : direct_reject(d, A.ks, A.n_slots, OPEN);  // direct mode
   if (st) {
     if (gl == 0) {
       atomicOr(A.err, 1u);

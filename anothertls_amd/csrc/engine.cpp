@@ -8,7 +8,8 @@
 // descriptors may stay device-resident (ATLS_FLAG_DEVICE_RECS) with no host-side partitioning.
 //
 // atls_seal / atls_open are the Cipher-trait drop-ins (crypto/ciphersuite.rs:12-31): one RAW
-// record through a process-default engine, with the same argument meaning and error codes.
+// record on the calling thread's engine (key cache, pinned staging), with the same argument
+// meaning and error codes.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -73,6 +74,7 @@ struct atls_engine {
   hipEvent_t ev_plan = nullptr, ev_side = nullptr;
   int cus = 256;
   uint32_t n_slots = 0;
+  std::vector<atls_key> keys;                // host copy of the installed slots (suite flags below)
   bool has_aes = false, has_chacha = false;  // suites present in the key table: skip idle kernels
   int aes_nr_mask = 0;                       // bit 0/1/2: AES slots with 10/12/14 rounds
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
@@ -346,26 +348,162 @@ int key_status(const atls_key& k) {
   return ATLS_INSUFFICIENT_SECURITY;
 }
 
-// ---- process-default engine for the Cipher-trait entry points -----------------------------
-std::mutex g_default_mu;
-atls_engine* g_default = nullptr;
-
-atls_engine* default_engine() {
-  std::lock_guard<std::mutex> lk(g_default_mu);
-  if (!g_default) {
-    const char* dv = std::getenv("ATLS_DEVICE");
-    g_default = atls_engine_create(dv ? std::atoi(dv) : 0);
+// Key slots [first, first + n) from host keys: the device key-setup kernel writes them in place
+// (the table grows, keeping the other slots); replace = the table becomes exactly these n slots.
+// Caller holds e->mu.
+int install_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t n, bool replace) {
+  int status = ATLS_OK;
+  for (uint32_t i = 0; i < n && status == ATLS_OK; i++) status = key_status(keys[i]);
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  const uint32_t total = replace ? n : std::max(e->n_slots, first + n);
+  const size_t need = sizeof(atls::KeySched) * (size_t)std::max<uint32_t>(total, 1);
+  if (need > e->ks.cap) {  // grow, keeping the installed slots
+    DevBuf grown;
+    if (!grown.reserve(std::max(need, 2 * e->ks.cap))) return ATLS_INTERNAL_ERROR;
+    if (!replace && e->n_slots &&
+        hipMemcpyAsync(grown.p, e->ks.p, sizeof(atls::KeySched) * (size_t)e->n_slots, hipMemcpyDeviceToDevice,
+                       e->stream) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
+    e->ks.release();
+    e->ks = grown;
+    grown.p = nullptr;
+    grown.cap = 0;
   }
-  return g_default;
+  if (!e->keys_stage.reserve(sizeof(atls_key) * (size_t)std::max<uint32_t>(n, 1))) return ATLS_INTERNAL_ERROR;
+  if (n && hipMemcpyAsync(e->keys_stage.p, keys, sizeof(atls_key) * (size_t)n, hipMemcpyHostToDevice, e->stream) !=
+               hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  if (atls_launch_key_setup((const atls_key*)e->keys_stage.p, n, (atls::KeySched*)e->ks.p + first, e->stream))
+    return ATLS_INTERNAL_ERROR;
+  if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  if (replace) e->keys.clear();
+  if (e->keys.size() < total) e->keys.resize(total);
+  std::copy(keys, keys + n, e->keys.begin() + first);
+  e->n_slots = total;
+  e->has_aes = e->has_chacha = false;
+  e->aes_nr_mask = 0;
+  for (const atls_key& k : e->keys) {
+    if (k.suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) {
+      e->has_chacha = true;
+      continue;
+    }
+    e->has_aes = true;  // AES-GCM, or an invalid slot the GCM kernel reports
+    if (key_status(k) == ATLS_OK) e->aes_nr_mask |= k.key_len == 16 ? 1 : k.key_len == 24 ? 2 : 4;
+  }
+  return status;
 }
 
-// Serialises the single-call entry points, which share the default engine's key slot 0.
-std::mutex& single_mu() {
-  static std::mutex m;
-  return m;
+// ---- Cipher-trait calls (atls_seal / atls_open / atls_aes_block) ------------------------------
+// The reference's record layer calls Cipher::encrypt / decrypt once per record from any thread
+// (Arc<dyn Cipher + Send + Sync>, ciphersuite.rs:78-87, record.rs:191-193). Each calling thread
+// gets its own engines (one per kind of key: AES-128 / -192 / -256 / ChaCha20, so every call is a
+// direct single-kernel batch) with a small key cache, pinned staging and its own streams: calls of
+// different threads run concurrently, and a repeated key costs no key setup (the reference
+// re-expands the key and recomputes H on every call, gcm.rs:52-56). Contexts of finished threads
+// go back to a pool for the next thread.
+constexpr uint32_t kCacheSlots = 16;
+
+struct KindEngine {
+  atls_engine* e = nullptr;
+  uint64_t stamp[kCacheSlots] = {};  // LRU clock per slot; 0 = free
+  uint64_t clock = 0;
+};
+
+struct SingleCtx {
+  KindEngine kinds[4];  // AES-128, AES-192, AES-256, ChaCha20-Poly1305
+  uint8_t* pin = nullptr;
+  size_t pin_cap = 0;
+  bool reserve_pin(size_t n) {
+    if (n <= pin_cap) return true;
+    if (pin) (void)hipHostFree(pin);
+    pin = nullptr;
+    pin_cap = 0;
+    size_t c = std::max<size_t>(n, size_t(1) << 16);
+    void* p = nullptr;
+    if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) return false;
+    pin = (uint8_t*)p;
+    pin_cap = c;
+    return true;
+  }
+};
+
+std::mutex g_pool_mu;
+std::vector<SingleCtx*>& ctx_pool() {
+  static std::vector<SingleCtx*>* pool = new std::vector<SingleCtx*>();  // never destroyed: outlives threads
+  return *pool;
 }
 
-// One Cipher::encrypt / decrypt call as a single RAW record.
+struct CtxLease {
+  SingleCtx* c = nullptr;
+  ~CtxLease() {
+    if (c) {
+      std::lock_guard<std::mutex> lk(g_pool_mu);
+      ctx_pool().push_back(c);
+    }
+  }
+};
+
+SingleCtx* this_thread_ctx() {
+  thread_local CtxLease lease;
+  if (!lease.c) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (!ctx_pool().empty()) {
+      lease.c = ctx_pool().back();
+      ctx_pool().pop_back();
+    } else {
+      lease.c = new (std::nothrow) SingleCtx();
+    }
+  }
+  return lease.c;
+}
+
+int kind_of(uint16_t suite, size_t key_len) {
+  if (suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) return 3;
+  return key_len == 16 ? 0 : key_len == 24 ? 1 : 2;
+}
+
+// Slot of this key in the thread's engine of its kind, installing it (LRU eviction) on a miss.
+int cached_slot(SingleCtx* c, uint16_t suite, const uint8_t* key, size_t key_len, atls_engine** eng, uint32_t* slot) {
+  KindEngine& k = c->kinds[kind_of(suite, key_len)];
+  if (!k.e) {
+    const char* dv = std::getenv("ATLS_DEVICE");
+    k.e = atls_engine_create(dv ? std::atoi(dv) : 0);
+    if (!k.e) return ATLS_INTERNAL_ERROR;
+  }
+  *eng = k.e;
+  uint32_t victim = 0;
+  for (uint32_t i = 0; i < kCacheSlots; i++) {
+    if (k.stamp[i] && i < k.e->keys.size() && k.e->keys[i].suite == suite && k.e->keys[i].key_len == key_len &&
+        std::memcmp(k.e->keys[i].key, key, key_len) == 0) {
+      k.stamp[i] = ++k.clock;
+      *slot = i;
+      return ATLS_OK;
+    }
+    if (k.stamp[i] < k.stamp[victim]) victim = i;
+  }
+  atls_key nk;
+  std::memset(&nk, 0, sizeof nk);
+  nk.suite = suite;
+  nk.key_len = (uint8_t)key_len;
+  nk.iv_len = 12;
+  std::memcpy(nk.key, key, key_len);
+  // slots fill in order, so a new slot never leaves a gap in the table
+  const uint32_t s = std::min<uint32_t>(victim, (uint32_t)k.e->keys.size());
+  int rc;
+  {
+    std::lock_guard<std::mutex> lk(k.e->mu);
+    rc = install_keys(k.e, s, &nk, 1, false);
+  }
+  if (rc) return rc;
+  k.stamp[s] = ++k.clock;
+  *slot = s;
+  return ATLS_OK;
+}
+
+// One Cipher::encrypt / decrypt call as a single RAW record on this thread's engine: the input,
+// nonce and AAD go through pinned staging into the engine's device buffers, one direct launch,
+// and the result comes back in one synchronisation.
 int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
            const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, const uint8_t* tag_in, size_t tag_len,
            uint8_t* out, uint8_t* tag_out) {
@@ -374,52 +512,72 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
     return ATLS_INSUFFICIENT_SECURITY;  // CipherSuite::get_cipher, ciphersuite.rs:78-87
   if (suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) {
     if (key_len != 32 || iv_len != 12) return ATLS_ILLEGAL_PARAMETER;  // poly1305.rs:20 unwrap
+    // ChaCha20::encrypt counts blocks as f32 (chacha20/cipher.rs:94), exact only below 2^24 B:
+    // longer inputs are refused rather than sealed differently from the reference
+    if (len >= (size_t(1) << 24)) return ATLS_ILLEGAL_PARAMETER;
   } else if (key_len != 16 && key_len != 24 && key_len != 32) {
     return ATLS_ILLEGAL_PARAMETER;  // gcm.rs:49 unwrap
   }
   if (iv_len > 255 || aad_len > 0xffff || len > 0xffffffffull) return ATLS_ILLEGAL_PARAMETER;
   if (open && tag_len != 16) return ATLS_BAD_RECORD_MAC;  // `T != auth_tag` with a wrong-length slice
-  atls_engine* e = default_engine();
-  if (!e) return ATLS_INTERNAL_ERROR;
-  atls_key k;
-  std::memset(&k, 0, sizeof k);
-  k.suite = suite;
-  k.key_len = (uint8_t)key_len;
-  k.iv_len = 12;
-  std::memcpy(k.key, key, key_len);
-  // One engine, one slot: serialise single calls (the batch API is the throughput path).
-  std::lock_guard<std::mutex> lk(single_mu());
-  int rc = atls_set_keys(e, &k, 1);
+  SingleCtx* c = this_thread_ctx();
+  if (!c) return ATLS_INTERNAL_ERROR;
+  atls_engine* e = nullptr;
+  uint32_t slot = 0;
+  int rc = cached_slot(c, suite, key, key_len, &e, &slot);
   if (rc) return rc;
-  std::vector<uint8_t> aux(iv_len + aad_len + 1);
-  if (iv_len) std::memcpy(aux.data(), iv, iv_len);
-  if (aad_len) std::memcpy(aux.data() + iv_len, aad, aad_len);
+  const size_t aux_len = iv_len + aad_len;
+  const size_t in_at = 0, aux_at = (len + 15) & ~size_t(15), tag_at = (aux_at + aux_len + 15) & ~size_t(15);
+  const size_t res_at = tag_at + 16, err_at = res_at + 8, total = err_at + 8;
+  if (!c->reserve_pin(total)) return ATLS_INTERNAL_ERROR;
+  uint8_t* h = c->pin;
+  if (len) std::memcpy(h + in_at, in, len);
+  if (iv_len) std::memcpy(h + aux_at, iv, iv_len);
+  if (aad_len) std::memcpy(h + aux_at + iv_len, aad, aad_len);
+  if (open) std::memcpy(h + tag_at, tag_in, 16);
   atls_rec r;
   std::memset(&r, 0, sizeof r);
   r.len = (uint32_t)len;
+  r.key_slot = slot;
   r.mode = ATLS_MODE_RAW;
   r.iv_len = (uint8_t)iv_len;
   r.aad_len = (uint16_t)aad_len;
-  std::vector<uint8_t> inb(len + 1), outb(len + 1);
-  if (len) std::memcpy(inb.data(), in, len);
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e) || !e->in.reserve(total + 16) || !e->out.reserve(len + 16) || !e->wgmax.reserve(4 * 512))
+    return ATLS_INTERNAL_ERROR;
+  uint8_t* d = (uint8_t*)e->in.p;
+  hipStream_t s = e->stream;
+  if (hipMemcpyAsync(d, h, res_at, hipMemcpyHostToDevice, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  // a RAW record's descriptor offsets are relative to the staged block above
+  r.in_off = in_at;
+  r.aux_off = 0;
+  if (!e->recs.reserve(sizeof(atls_rec)) ||
+      hipMemcpyAsync(e->recs.p, &r, sizeof r, hipMemcpyHostToDevice, s) != hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  uint8_t* dout = (uint8_t*)e->out.p;
+  atls_open_result* dres = (atls_open_result*)(d + res_at);
+  if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  rc = launch_records(e, open, (const atls_rec*)e->recs.p, 1, d, d + aux_at, dout, d + tag_at, d + tag_at, dres, s, 0);
+  if (rc) return rc;
+  if (len && hipMemcpyAsync(h + in_at, dout, len, hipMemcpyDeviceToHost, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  if (hipMemcpyAsync(h + tag_at, d + tag_at, 16 + sizeof(atls_open_result), hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipMemcpyAsync(h + err_at, e->err.p, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  uint32_t err = 0;
+  std::memcpy(&err, h + err_at, 4);
+  if (err) return ATLS_ILLEGAL_PARAMETER;
   if (!open) {
-    uint8_t tg[16];
-    rc = atls_seal_batch(e, &r, 1, inb.data(), aux.data(), outb.data(), tg, 0);
-    if (rc) return rc;
-    if (len) std::memcpy(out, outb.data(), len);
-    std::memcpy(tag_out, tg, 16);
+    if (len) std::memcpy(out, h + in_at, len);
+    std::memcpy(tag_out, h + tag_at, 16);
     return ATLS_OK;
   }
-  uint8_t tg[16];
-  std::memcpy(tg, tag_in, 16);
   atls_open_result res;
-  rc = atls_open_batch(e, &r, 1, inb.data(), aux.data(), tg, outb.data(), &res, 0);
-  if (rc) return rc;
+  std::memcpy(&res, h + res_at, sizeof res);
   if (res.status != ATLS_OK) {
     if (len) std::memset(out, 0, len);  // no unauthenticated plaintext leaves (reference returns Err)
     return res.status;
   }
-  if (len) std::memcpy(out, outb.data(), len);
+  if (len) std::memcpy(out, h + in_at, len);
   return ATLS_OK;
 }
 
@@ -487,30 +645,15 @@ void* atls_engine_stream(atls_engine* e) { return e ? (void*)e->stream : nullptr
 
 int atls_set_keys(atls_engine* e, const atls_key* keys, uint32_t n) {
   if (!e || (!keys && n)) return ATLS_INTERNAL_ERROR;
-  int status = ATLS_OK;
-  for (uint32_t i = 0; i < n && status == ATLS_OK; i++) status = key_status(keys[i]);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
-  if (!e->ks.reserve(sizeof(atls::KeySched) * (size_t)std::max<uint32_t>(n, 1)) ||
-      !e->keys_stage.reserve(sizeof(atls_key) * (size_t)std::max<uint32_t>(n, 1)))
-    return ATLS_INTERNAL_ERROR;
-  if (n && hipMemcpyAsync(e->keys_stage.p, keys, sizeof(atls_key) * (size_t)n, hipMemcpyHostToDevice, e->stream) !=
-               hipSuccess)
-    return ATLS_INTERNAL_ERROR;
-  if (atls_launch_key_setup((const atls_key*)e->keys_stage.p, n, e->ks.p, e->stream)) return ATLS_INTERNAL_ERROR;
-  if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
-  e->n_slots = n;
-  e->has_aes = e->has_chacha = false;
-  e->aes_nr_mask = 0;
-  for (uint32_t i = 0; i < n; i++) {
-    if (keys[i].suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) {
-      e->has_chacha = true;
-      continue;
-    }
-    e->has_aes = true;  // AES-GCM, or an invalid slot the GCM kernel reports
-    if (key_status(keys[i]) == ATLS_OK) e->aes_nr_mask |= keys[i].key_len == 16 ? 1 : keys[i].key_len == 24 ? 2 : 4;
-  }
-  return status;
+  return install_keys(e, 0, keys, n, true);
+}
+
+int atls_update_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t n) {
+  if (!e || (!keys && n)) return ATLS_INTERNAL_ERROR;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (first > e->n_slots) return ATLS_ILLEGAL_PARAMETER;  // slots stay contiguous
+  return install_keys(e, first, keys, n, false);
 }
 
 int atls_seal_batch(atls_engine* e, const atls_rec* recs, uint32_t n, const void* in, const void* aux, void* out,
@@ -587,18 +730,13 @@ int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* 
 
 int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_t in[16], uint8_t out[16]) {
   if (key_len != 16 && key_len != 24 && key_len != 32) return ATLS_ILLEGAL_PARAMETER;  // AES::init key sizes
-  atls_engine* e = default_engine();
-  if (!e) return ATLS_INTERNAL_ERROR;
-  atls_key k;
-  std::memset(&k, 0, sizeof k);
-  k.suite = ATLS_TLS_AES_128_GCM_SHA256;  // any AES suite: the slot only carries the key
-  k.key_len = (uint8_t)key_len;
-  k.iv_len = 12;
-  std::memcpy(k.key, key, key_len);
-  std::lock_guard<std::mutex> lk(single_mu());
-  int rc = atls_set_keys(e, &k, 1);
-  if (rc) return rc;
-  return atls_aes_blocks(e, decrypt, 0, in, out, 1, 0);
+  SingleCtx* c = this_thread_ctx();
+  if (!c) return ATLS_INTERNAL_ERROR;
+  atls_engine* e = nullptr;
+  uint32_t slot = 0;
+  // any AES suite: the slot only carries the key (the thread's engine of this key size)
+  const int rc = cached_slot(c, ATLS_TLS_AES_128_GCM_SHA256, key, key_len, &e, &slot);
+  return rc ? rc : atls_aes_blocks(e, decrypt, slot, in, out, 1, 0);
 }
 
 }  // extern "C"

@@ -516,7 +516,7 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
     d.len = uni(d.len);
     d.mode = (uint8_t)uni(d.mode);
     if (!A.idx) {  // direct mode: reject as the plan would
-      const uint32_t st = uni(direct_reject(d, A.ks, A.n_slots));
+      const uint32_t st = uni(direct_reject(d, A.ks, A.n_slots, OPEN));
       if (st) {
         if (lane == 0) {
           atomicOr(A.err, 1u);

@@ -34,13 +34,22 @@ struct WorkList {
   __device__ __forceinline__ uint32_t record(uint32_t pos) const { return idx ? idx[P->off[list] + pos] : pos; }
 };
 
+// ChaCha20::encrypt counts its 64-byte blocks as (len as f32 / 64.0).ceil() (chacha20/cipher.rs:94),
+// exact only while the AEAD input is below 2^24 bytes. Longer ChaCha20-Poly1305 records are
+// refused (ILLEGAL_PARAMETER) instead of being sealed differently from the reference.
+__device__ __forceinline__ bool chacha_len_ok(const atls_rec& d, bool open) {
+  const uint64_t aead = (uint64_t)d.len + ((!open && d.mode != ATLS_MODE_RAW) ? 1u : 0u);  // + type byte
+  return aead < (1ull << 24);
+}
+
 // Direct mode: the status a record gets in place of sealing / opening (0 = process it), as
 // plan_key would give it (plan.hip).
-__device__ __forceinline__ uint32_t direct_reject(const atls_rec& d, const KeySched* ks, uint32_t n_slots) {
+__device__ __forceinline__ uint32_t direct_reject(const atls_rec& d, const KeySched* ks, uint32_t n_slots, bool open) {
   if (d.key_slot >= n_slots || d.mode > ATLS_MODE_WIRE) return ATLS_ILLEGAL_PARAMETER;
   const KeySched* k = ks + d.key_slot;
   const uint32_t suite = k->suite;
-  if (suite == (uint32_t)kSuiteChacha) return (!k->valid || (d.mode == ATLS_MODE_RAW && d.iv_len != 12)) ? ATLS_ILLEGAL_PARAMETER : 0;
+  if (suite == (uint32_t)kSuiteChacha)
+    return (!k->valid || (d.mode == ATLS_MODE_RAW && d.iv_len != 12) || !chacha_len_ok(d, open)) ? ATLS_ILLEGAL_PARAMETER : 0;
   if (suite == (uint32_t)kSuiteAes128 || suite == (uint32_t)kSuiteAes256) return k->valid ? 0 : ATLS_ILLEGAL_PARAMETER;
   return ATLS_INSUFFICIENT_SECURITY;
 }

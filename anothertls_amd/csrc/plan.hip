@@ -19,7 +19,7 @@ namespace atls {
 
 // Work-list key of record i, or kPlanReject (status in *st).
 __device__ __forceinline__ uint32_t plan_key(const atls_rec* recs, uint32_t i, const KeySched* ks, uint32_t n_slots,
-                                             uint8_t* st) {
+                                             uint8_t* st, bool open) {
   const atls_rec d = recs[i];
   *st = ATLS_ILLEGAL_PARAMETER;
   if (d.key_slot >= n_slots || d.mode > ATLS_MODE_WIRE) return kPlanReject;
@@ -28,6 +28,7 @@ __device__ __forceinline__ uint32_t plan_key(const atls_rec* recs, uint32_t i, c
   uint32_t list;
   if (suite == (uint32_t)kSuiteChacha) {
     if (!valid || (d.mode == ATLS_MODE_RAW && d.iv_len != 12)) return kPlanReject;  // cipher.rs:19
+    if (!chacha_len_ok(d, open)) return kPlanReject;                                 // cipher.rs:94
     list = kListChacha;
   } else if (suite == (uint32_t)kSuiteAes128 || suite == (uint32_t)kSuiteAes256) {
     if (!valid) return kPlanReject;
@@ -60,7 +61,7 @@ __global__ __launch_bounds__(256) void plan_count(const atls_rec* recs, uint32_t
   plan_chunk(n, lo, hi);
   for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
     uint8_t st = 0;
-    const uint32_t key = plan_key(recs, i, ks, n_slots, &st);
+    const uint32_t key = plan_key(recs, i, ks, n_slots, &st, open != 0);
     keys[i] = (uint8_t)key;
     if (key == kPlanReject) {
       atomicOr(err, 1u);

@@ -124,7 +124,9 @@ typedef struct atls_engine atls_engine;
  * atls_seal  <- Cipher::encrypt: out = ciphertext (len B), tag = 16 B.
  * atls_open  <- Cipher::decrypt: out = plaintext (len B) or ATLS_BAD_RECORD_MAC (a tag of the
  *               wrong length is a mismatch, as `T != auth_tag` is in the reference).
- * Host pointers; run on the process-default engine (device 0 or $ATLS_DEVICE). Reentrant. */
+ * Host pointers; device 0 or $ATLS_DEVICE. Reentrant and concurrent (Cipher is Send + Sync): each
+ * calling thread has its own engines and streams, and keeps the device key schedules of its last
+ * 16 keys per key size, so repeated keys cost no key setup (finished threads' contexts are reused). */
 int atls_seal(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
               const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, uint8_t* out,
               uint8_t tag[16]);
@@ -142,6 +144,9 @@ void* atls_engine_stream(atls_engine* e);
 /* Install n key slots (host array). Runs the device key-setup kernel: AES round keys, H = E_K(0),
  * H^1..H^64 and the GHASH table seeds; ChaCha keys are used as given. Replaces previous slots. */
 int atls_set_keys(atls_engine* e, const atls_key* keys, uint32_t n);
+/* Install n key slots at [first, first + n) without touching the others (connections come and go);
+ * first <= the current slot count (slots stay contiguous; the table grows as needed). */
+int atls_update_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t n);
 
 /* Seal / open n records. */
 int atls_seal_batch(atls_engine* e, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
@@ -163,7 +168,7 @@ int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, siz
  * ATLS_FLAG_NO_SYNC as for the batches. */
 int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* in, void* out, size_t nblocks,
                     uint32_t flags);
-/* One block with a raw key (16/24/32 B) on the process-default engine. */
+/* One block with a raw key (16/24/32 B) on the calling thread's engine (as atls_seal). */
 int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_t in[16], uint8_t out[16]);
 
 /* ---- Multi-GPU batches (one process, several devices), SURVEY.md §8(b)/(e) ----------------

@@ -1,0 +1,116 @@
+"""The Cipher-trait drop-in (atls_seal / atls_open) as the reference's record layer uses it: one
+call per record, from any thread (Arc<dyn Cipher + Send + Sync>, crypto/ciphersuite.rs:78-87,
+net/record.rs:191-193): concurrent calls from several threads, the per-thread key cache across
+evictions, the ChaCha20 f32 block-count limit (chacha20/cipher.rs:94), and atls_update_keys."""
+import os
+import random
+import threading
+
+import numpy as np
+import pytest
+
+import anothertls_amd as atls
+import oracle as ora
+from anothertls_amd import workload
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(rng, keys):
+    suite, key = rng.choice(keys)
+    n = rng.choice([0, 1, 15, 16, 17, 63, 64, 127, 1536, 1537, 4096, 16385])
+    iv = bytes(rng.getrandbits(8) for _ in range(12))
+    aad = bytes(rng.getrandbits(8) for _ in range(rng.choice([0, 5, 13])))
+    pt = bytes(rng.getrandbits(8) for _ in range(n))
+    return suite, key, iv, aad, pt
+
+
+def test_concurrent_threads_vs_oracle():
+    rng0 = random.Random(5)
+    keys = [(s, bytes(rng0.getrandbits(8) for _ in range(kl))) for s, kl in
+            [(0x1301, 16), (0x1301, 16), (0x1302, 32), (0x1301, 24), (0x1303, 32), (0x1303, 32)]]
+    errors = []
+
+    def worker(t):
+        rng = random.Random(100 + t)
+        try:
+            for _ in range(40):
+                suite, key, iv, aad, pt = _case(rng, keys)
+                c = atls.CipherSuite(suite).get_cipher()
+                ct, tag = c.encrypt(key, iv, pt, aad)
+                rc, ect, etag = ora.cipher_encrypt(suite, key, iv, pt, aad)
+                assert rc == 0 and ct == ect and tag == etag, (t, suite, len(pt))
+                assert c.decrypt(key, iv, ct, aad, tag) == pt
+                with pytest.raises(atls.TlsError) as e:
+                    c.decrypt(key, iv, ct, aad, bytes([tag[0] ^ 1]) + tag[1:])
+                assert e.value.code == 20
+        except BaseException as exc:  # noqa: BLE001 -- reported by the main thread
+            errors.append(exc)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(120)
+    assert not errors, errors[:3]
+
+
+def test_key_cache_eviction_cycles():
+    rng = random.Random(9)
+    keys = [bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(40)]  # > 16 cached slots
+    c = atls.Gcm()
+    for rnd in range(2):
+        for i, k in enumerate(keys):
+            pt = bytes([i, rnd]) * 100
+            iv = bytes([rnd]) * 12
+            ct, tag = c.encrypt(k, iv, pt, b"hdr")
+            rc, ect, etag = ora.gcm_encrypt(k, iv, pt, b"hdr")
+            assert rc == 0 and (ct, tag) == (ect, etag), (rnd, i)
+
+
+def test_chacha_f32_block_count_limit():
+    key, iv = bytes(range(32)), bytes(12)
+    c = atls.Poly1305()
+    with pytest.raises(atls.TlsError) as e:  # 2^24 + 1: the reference's f32 ceil drops the last byte
+        c.encrypt(key, iv, bytes(2**24 + 1))
+    assert e.value.code == 47
+    # the largest accepted length is exact in f32 and matches the oracle
+    pt = np.random.default_rng(1).integers(0, 256, 2**24 - 1, dtype=np.uint8).tobytes()
+    ct, tag = c.encrypt(key, iv, pt, b"")
+    rc, ect, etag = ora.chacha_poly_encrypt(key, iv, pt, b"")
+    assert rc == 0 and ct == ect and tag == etag
+    # batch path: a TLS seal of 2^24 - 1 content bytes is a 2^24-byte AEAD input -> refused
+    eng = atls.Engine(0)
+    b = workload.tls_batch(2, np.array([100, 2**24 - 1], np.uint64), 0x1303, n_keys=1)
+    eng.set_keys(b["keys"])
+    inbuf = np.zeros(b["in_bytes"] + 16, np.uint8)
+    out = np.zeros(b["out_bytes"] + 16, np.uint8)
+    with pytest.raises(atls.TlsError) as e:
+        eng.seal_batch(b["recs"], inbuf, np.zeros(16, np.uint8), out, np.zeros(32, np.uint8))
+    assert e.value.code == 47
+    eng.close()
+
+
+def test_update_keys_keeps_other_slots():
+    from test_gpu_parity import fill_payload, oracle_keys, oracle_recs
+
+    def suites(k):
+        return np.array([0x1301, 0x1303, 0x1302, 0x1301][:k], np.uint16)
+
+    b = workload.tls_batch(8, 3000, suites, n_keys=4)
+    eng = atls.Engine(0)
+    eng.set_keys(b["keys"][:3])
+    new = workload.make_keys(2, np.array([0x1302, 0x1301], np.uint16), seed=77)
+    eng.update_keys(2, new)  # replaces slot 2, appends slot 3
+    keys = b["keys"].copy()
+    keys[2:4] = new
+    inbuf = fill_payload(b, 4)
+    out = np.zeros(b["out_bytes"] + 16, np.uint8)
+    tags = np.zeros(16 * 8, np.uint8)
+    eng.seal_batch(b["recs"], inbuf, np.zeros(16, np.uint8), out, tags)
+    oout, otags = np.zeros_like(out), np.zeros_like(tags)
+    assert ora.seal_batch(oracle_keys(keys), oracle_recs(b["recs"]), inbuf, np.zeros(16, np.uint8), oout, otags, 4) == 0
+    assert np.array_equal(tags, otags) and np.array_equal(out, oout)
+    with pytest.raises(atls.TlsError):
+        eng.update_keys(9, new)  # would leave a gap
+    eng.close()
