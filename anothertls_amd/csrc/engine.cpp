@@ -40,6 +40,10 @@ extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs
                                   uint32_t n_slots, const uint32_t* wgmax, uint32_t n_wgmax, int grid, hipStream_t s);
 extern "C" int atls_launch_prep(const atls_rec* recs, uint32_t n, uint32_t* err, uint32_t* wgmax, hipStream_t s,
                                 uint32_t* n_wg);
+extern "C" int atls_launch_hash(int op, uint32_t hl, const uint8_t* data, const atls_span* keys, const atls_span* msgs,
+                                uint32_t n, uint32_t out_len, uint8_t* out, hipStream_t s);
+extern "C" int atls_launch_key_schedule(uint32_t hl, const uint8_t* shared, uint32_t shared_len, const uint8_t* hello,
+                                        const uint8_t* fin, uint32_t n, uint8_t* out, hipStream_t s);
 extern "C" int atls_launch_derive(uint16_t suite, const uint8_t* secrets, uint32_t secret_len, uint32_t n,
                                   atls_key* out, hipStream_t s);
 
@@ -696,6 +700,60 @@ int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, siz
   if (hipMemcpyAsync(out_keys, e->dkeys.p, sizeof(atls_key) * (size_t)n, hipMemcpyDeviceToHost, e->stream) != hipSuccess)
     return ATLS_INTERNAL_ERROR;
   return hipStreamSynchronize(e->stream) == hipSuccess ? ATLS_OK : ATLS_INTERNAL_ERROR;
+}
+
+int atls_hash_batch(atls_engine* e, int op, uint32_t hash_len, const uint8_t* data, size_t data_len,
+                    const atls_span* keys, const atls_span* msgs, uint32_t n, uint32_t out_len, uint8_t* out) {
+  if (!e) return ATLS_INTERNAL_ERROR;
+  if ((hash_len != 32 && hash_len != 48) || op < ATLS_HASH_SHA || op > ATLS_HASH_HKDF_EXPAND || !msgs ||
+      (op != ATLS_HASH_SHA && !keys))
+    return ATLS_ILLEGAL_PARAMETER;
+  if (op == ATLS_HASH_HKDF_EXPAND ? out_len > 255u * hash_len : out_len != hash_len)
+    return ATLS_ILLEGAL_PARAMETER;  // hkdf.rs:38 returns None past 255 * HashLen
+  for (uint32_t i = 0; i < n; i++) {  // every span inside data
+    if (msgs[i].off + msgs[i].len > data_len) return ATLS_ILLEGAL_PARAMETER;
+    if (op != ATLS_HASH_SHA && keys[i].off + keys[i].len > data_len) return ATLS_ILLEGAL_PARAMETER;
+  }
+  if (n == 0) return ATLS_OK;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  hipStream_t s = e->stream;
+  const size_t span_bytes = sizeof(atls_span) * (size_t)n, out_bytes = (size_t)out_len * n;
+  if (!e->secrets.reserve(data_len + 2 * span_bytes + 64) || !e->dkeys.reserve(out_bytes + 16)) return ATLS_INTERNAL_ERROR;
+  uint8_t* d = (uint8_t*)e->secrets.p;
+  atls_span* dk = (atls_span*)(d + ((data_len + 15) & ~size_t(15)));
+  atls_span* dm = dk + n;
+  if ((data_len && hipMemcpyAsync(d, data, data_len, hipMemcpyHostToDevice, s) != hipSuccess) ||
+      (keys && hipMemcpyAsync(dk, keys, span_bytes, hipMemcpyHostToDevice, s) != hipSuccess) ||
+      hipMemcpyAsync(dm, msgs, span_bytes, hipMemcpyHostToDevice, s) != hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  if (atls_launch_hash(op, hash_len, d, keys ? dk : nullptr, dm, n, out_len, (uint8_t*)e->dkeys.p, s)) return ATLS_INTERNAL_ERROR;
+  if (hipMemcpyAsync(out, e->dkeys.p, out_bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  return hipStreamSynchronize(s) == hipSuccess ? ATLS_OK : ATLS_INTERNAL_ERROR;
+}
+
+int atls_key_schedule(atls_engine* e, uint32_t hash_len, const uint8_t* shared, size_t shared_len,
+                      const uint8_t* hello_hashes, const uint8_t* handshake_hashes, uint32_t n, uint8_t* out) {
+  if (!e) return ATLS_INTERNAL_ERROR;
+  if ((hash_len != 32 && hash_len != 48) || !shared || !hello_hashes || shared_len > 1024) return ATLS_ILLEGAL_PARAMETER;
+  if (n == 0) return ATLS_OK;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  hipStream_t s = e->stream;
+  const size_t sb = shared_len * n, hb = (size_t)hash_len * n, ob = 5 * (size_t)hash_len * n;
+  const size_t a0 = (sb + 15) & ~size_t(15), a1 = a0 + ((hb + 15) & ~size_t(15));
+  if (!e->secrets.reserve(a1 + hb + 16) || !e->dkeys.reserve(ob + 16)) return ATLS_INTERNAL_ERROR;
+  uint8_t* d = (uint8_t*)e->secrets.p;
+  if (hipMemcpyAsync(d, shared, sb, hipMemcpyHostToDevice, s) != hipSuccess ||
+      hipMemcpyAsync(d + a0, hello_hashes, hb, hipMemcpyHostToDevice, s) != hipSuccess ||
+      (handshake_hashes && hipMemcpyAsync(d + a1, handshake_hashes, hb, hipMemcpyHostToDevice, s) != hipSuccess) ||
+      hipMemsetAsync(e->dkeys.p, 0, ob, s) != hipSuccess)
+    return ATLS_INTERNAL_ERROR;
+  if (atls_launch_key_schedule(hash_len, d, (uint32_t)shared_len, d + a0, handshake_hashes ? d + a1 : nullptr, n,
+                               (uint8_t*)e->dkeys.p, s))
+    return ATLS_INTERNAL_ERROR;
+  if (hipMemcpyAsync(out, e->dkeys.p, ob, hipMemcpyDeviceToHost, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  return hipStreamSynchronize(s) == hipSuccess ? ATLS_OK : ATLS_INTERNAL_ERROR;
 }
 
 int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* in, void* out, size_t nblocks,

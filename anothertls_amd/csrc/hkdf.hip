@@ -1,8 +1,9 @@
-// Batched traffic-key derivation on the device: Key::from_hkdf (net/key_schedule.rs:40-50).
-// For each traffic secret (the HKDF PRK): key = HKDF-Expand-Label(secret, "key", "", key_len),
-// iv = HKDF-Expand-Label(secret, "iv", "", 12) (key_schedule.rs:20-29, hash/hkdf.rs:35-65,
-// hash/hmac.rs:29-78, hash/sha256.rs / sha384.rs). One thread per connection; output goes
-// straight into atls_key slots for atls_set_keys.
+// The hash side of the path on the device: SHA-256 / SHA-384
+// (hash/sha256.rs, sha384.rs), HMAC (hash/hmac.rs:29-78), HKDF extract / expand (hash/hkdf.rs:24-65),
+// the TLS 1.3 secret chain (KeySchedule::do_key_schedule, net/key_schedule.rs:170-222, and the
+// application secrets, :87-114) and traffic-key derivation (Key::from_hkdf, :40-50) straight
+// into atls_key slots for atls_set_keys. One thread per item (connection): this runs a few
+// times per connection, not per record.
 #include "atls_dev.h"
 
 namespace atls {
@@ -81,44 +82,121 @@ __device__ void sha384_block(uint64_t st[8], const uint8_t* p) {
   st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-// SHA-256 / SHA-384 of a short message (len <= 255). Standard padding; the reference writes only
-// 7 (15) of the 8 (16) length bytes (sha256.rs:60-62, sha384.rs:60-62), identical below 2^56 bits.
-__device__ void sha_small(int hl, const uint8_t* m, uint32_t len, uint8_t* out) {
-  const uint32_t bs = hl == 48 ? 128u : 64u;
-  uint8_t buf[384];
-  uint32_t tot = ((len + 1 + (bs == 128 ? 16 : 8) + bs - 1) / bs) * bs;
-  for (uint32_t i = 0; i < tot; i++) buf[i] = i < len ? m[i] : 0;
-  buf[len] = 0x80;
-  const uint64_t bits = (uint64_t)len * 8;
-  for (int i = 0; i < 8; i++) buf[tot - 1 - i] = (uint8_t)(bits >> (8 * i));
+// ---- streaming SHA-256 / SHA-384 (hash/sha256.rs, hash/sha384.rs) ----------------------------
+// One thread per message. The reference pads with 0x80, zeros and the bit length written into only
+// 7 (SHA-256, sha256.rs:60-62) or 15 (SHA-384) of the 8 / 16 length bytes; below 2^56 bits that is
+// the standard length field, which is what this writes.
+struct ShaCtx {
+  int hl;  // 32 (SHA-256) or 48 (SHA-384)
+  uint32_t s32[8];
+  uint64_t s64[8];
+  uint8_t buf[128];
+  uint32_t blen;
+  uint64_t total;
+};
+
+__device__ void sha_init(ShaCtx& c, int hl) {
+  c.hl = hl;
+  c.blen = 0;
+  c.total = 0;
   if (hl == 32) {
-    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-    for (uint32_t o = 0; o < tot; o += 64) sha256_block(st, buf + o);
-    for (int i = 0; i < 32; i++) out[i] = (uint8_t)(st[i >> 2] >> (8 * (3 - (i & 3))));
+    const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    for (int i = 0; i < 8; i++) c.s32[i] = iv[i];
   } else {
-    uint64_t st[8] = {0xcbbb9d5dc1059ed8ull, 0x629a292a367cd507ull, 0x9159015a3070dd17ull, 0x152fecd8f70e5939ull,
-                      0x67332667ffc00b31ull, 0x8eb44a8768581511ull, 0xdb0c2e0d64f98fa7ull, 0x47b5481dbefa4fa4ull};
-    for (uint32_t o = 0; o < tot; o += 128) sha384_block(st, buf + o);
-    for (int i = 0; i < 48; i++) out[i] = (uint8_t)(st[i >> 3] >> (8 * (7 - (i & 7))));
+    const uint64_t iv[8] = {0xcbbb9d5dc1059ed8ull, 0x629a292a367cd507ull, 0x9159015a3070dd17ull, 0x152fecd8f70e5939ull,
+                            0x67332667ffc00b31ull, 0x8eb44a8768581511ull, 0xdb0c2e0d64f98fa7ull, 0x47b5481dbefa4fa4ull};
+    for (int i = 0; i < 8; i++) c.s64[i] = iv[i];
   }
 }
 
-// HMAC (hash/hmac.rs:29-78) with a key of at most 64 bytes (a TLS traffic secret: 32 or 48).
-__device__ void hmac_small(int hl, const uint8_t* key, uint32_t klen, const uint8_t* msg, uint32_t mlen, uint8_t* out) {
-  const uint32_t size = hl == 48 ? 128u : 64u;
-  uint8_t buf[128 + 64];
-  for (uint32_t i = 0; i < size; i++) buf[i] = (i < klen ? key[i] : 0) ^ 0x36;
-  for (uint32_t i = 0; i < mlen; i++) buf[size + i] = msg[i];
-  uint8_t inner[48];
-  sha_small(hl, buf, size + mlen, inner);
-  for (uint32_t i = 0; i < size; i++) buf[i] = (i < klen ? key[i] : 0) ^ 0x5c;
-  for (int i = 0; i < hl; i++) buf[size + i] = inner[i];
-  sha_small(hl, buf, size + (uint32_t)hl, out);
+__device__ void sha_update(ShaCtx& c, const uint8_t* p, uint64_t n) {
+  const uint32_t bs = c.hl == 48 ? 128u : 64u;
+  c.total += n;
+  for (uint64_t i = 0; i < n; i++) {
+    c.buf[c.blen++] = p[i];
+    if (c.blen == bs) {
+      if (c.hl == 32) sha256_block(c.s32, c.buf);
+      else sha384_block(c.s64, c.buf);
+      c.blen = 0;
+    }
+  }
 }
 
-// HKDF-Expand-Label(secret, label, "", L) for L <= HashLen: T(1) = HMAC(secret, info || 0x01).
-__device__ void expand_label(int hl, const uint8_t* secret, const char* label, uint32_t llen, uint32_t L, uint8_t* out) {
-  uint8_t info[32];
+__device__ void sha_final(ShaCtx& c, uint8_t* out) {
+  const uint32_t bs = c.hl == 48 ? 128u : 64u, lb = bs == 128 ? 16u : 8u;
+  const uint64_t bits = c.total * 8;
+  uint8_t pad[144];
+  const uint32_t used = c.blen;
+  const uint32_t padn = (used + 1 + lb <= bs) ? bs - used : 2 * bs - used;
+  for (uint32_t i = 0; i < padn; i++) pad[i] = 0;
+  pad[0] = 0x80;
+  for (int i = 0; i < 8; i++) pad[padn - 1 - i] = (uint8_t)(bits >> (8 * i));
+  const uint64_t keep = c.total;
+  sha_update(c, pad, padn);
+  c.total = keep;
+  if (c.hl == 32) {
+    for (int i = 0; i < 32; i++) out[i] = (uint8_t)(c.s32[i >> 2] >> (8 * (3 - (i & 3))));
+  } else {
+    for (int i = 0; i < 48; i++) out[i] = (uint8_t)(c.s64[i >> 3] >> (8 * (7 - (i & 7))));
+  }
+}
+
+__device__ void sha_x(int hl, const uint8_t* m, uint64_t len, uint8_t* out) {  // hash/mod.rs:37-42
+  ShaCtx c;
+  sha_init(c, hl);
+  sha_update(c, m, len);
+  sha_final(c, out);
+}
+
+// HMAC (hash/hmac.rs:29-78) over the concatenation of up to three message parts. Keys longer than
+// 64 bytes are hashed first for BOTH hashes (hmac.rs:41-49), which differs from RFC 2104 for
+// SHA-384 keys of 65..128 bytes; the padded key is 64 (SHA-256) or 128 (SHA-384) bytes.
+__device__ void hmac_parts(int hl, const uint8_t* key, uint64_t klen, const uint8_t* m0, uint64_t l0, const uint8_t* m1,
+                           uint64_t l1, const uint8_t* m2, uint64_t l2, uint8_t* out) {
+  const uint32_t size = hl == 48 ? 128u : 64u;
+  uint8_t kb[128], hk[48];
+  if (klen > 64) {
+    sha_x(hl, key, klen, hk);
+    key = hk;
+    klen = (uint64_t)hl;
+  }
+  for (uint32_t i = 0; i < size; i++) kb[i] = (i < klen ? key[i] : 0) ^ 0x36;
+  ShaCtx c;
+  sha_init(c, hl);
+  sha_update(c, kb, size);
+  sha_update(c, m0, l0);
+  sha_update(c, m1, l1);
+  sha_update(c, m2, l2);
+  uint8_t inner[48];
+  sha_final(c, inner);
+  for (uint32_t i = 0; i < size; i++) kb[i] ^= 0x36 ^ 0x5c;
+  sha_init(c, hl);
+  sha_update(c, kb, size);
+  sha_update(c, inner, (uint64_t)hl);
+  sha_final(c, out);
+}
+
+// HKDF-Expand (hash/hkdf.rs:35-65): T(i) = HMAC(PRK, T(i-1) || info || i) with a u8 counter,
+// out_len <= 255 * HashLen (checked by the caller).
+__device__ void hkdf_expand(int hl, const uint8_t* prk, uint64_t prk_len, const uint8_t* info, uint64_t info_len,
+                            uint8_t* out, uint32_t out_len) {
+  uint8_t t[48];
+  uint32_t got = 0, tl = 0;
+  uint8_t i = 0;
+  while (got < out_len) {
+    i++;
+    hmac_parts(hl, prk, prk_len, t, tl, info, info_len, &i, 1, t);
+    tl = (uint32_t)hl;
+    const uint32_t need = min(out_len - got, (uint32_t)hl);
+    for (uint32_t j = 0; j < need; j++) out[got + j] = t[j];
+    got += need;
+  }
+}
+
+// get_hkdf_expand_label (net/key_schedule.rs:20-29): {len_hi, len_lo, 6 + |label|, "tls13 " label,
+// |ctx|, ctx}. Returns the length.
+__device__ uint32_t expand_label_info(const char* label, uint32_t llen, const uint8_t* ctx, uint32_t clen, uint32_t L,
+                                      uint8_t* info) {
   uint32_t p = 0;
   info[p++] = (uint8_t)(L >> 8);
   info[p++] = (uint8_t)L;
@@ -126,11 +204,16 @@ __device__ void expand_label(int hl, const uint8_t* secret, const char* label, u
   const char* pre = "tls13 ";
   for (int i = 0; i < 6; i++) info[p++] = (uint8_t)pre[i];
   for (uint32_t i = 0; i < llen; i++) info[p++] = (uint8_t)label[i];
-  info[p++] = 0;  // empty context
-  info[p++] = 1;  // HKDF counter i = 1 (hkdf.rs:55-59)
-  uint8_t t[48];
-  hmac_small(hl, secret, (uint32_t)hl, info, p, t);
-  for (uint32_t i = 0; i < L; i++) out[i] = t[i];
+  info[p++] = (uint8_t)clen;
+  for (uint32_t i = 0; i < clen; i++) info[p++] = ctx[i];
+  return p;
+}
+
+__device__ void expand_label(int hl, const uint8_t* secret, const char* label, uint32_t llen, const uint8_t* ctx,
+                             uint32_t clen, uint32_t L, uint8_t* out) {
+  uint8_t info[128];
+  const uint32_t il = expand_label_info(label, llen, ctx, clen, L, info);
+  hkdf_expand(hl, secret, (uint64_t)hl, info, il, out, L);
 }
 
 __global__ void derive_kernel(uint16_t suite, const uint8_t* __restrict__ secrets, uint32_t hl, uint32_t n,
@@ -143,12 +226,77 @@ __global__ void derive_kernel(uint16_t suite, const uint8_t* __restrict__ secret
   k.suite = suite;
   k.key_len = suite == kSuiteAes128 ? 16 : 32;  // CipherSuite::get_key_and_iv_len, ciphersuite.rs:69-77
   k.iv_len = 12;
-  expand_label((int)hl, sec, "key", 3, k.key_len, k.key);
-  expand_label((int)hl, sec, "iv", 2, 12, k.static_iv);
+  expand_label((int)hl, sec, "key", 3, nullptr, 0, k.key_len, k.key);  // Key::from_hkdf, key_schedule.rs:40-50
+  expand_label((int)hl, sec, "iv", 2, nullptr, 0, 12, k.static_iv);
   out[i] = k;
 }
 
+// Batched hashing primitives (include/atls.h atls_hash_batch): item i hashes data + msg[i] (and
+// keys with data + key[i]); output at out + i * out_len.
+__global__ void hash_kernel(int op, uint32_t hl, const uint8_t* __restrict__ data, const atls_span* __restrict__ keys,
+                            const atls_span* __restrict__ msgs, uint32_t n, uint32_t out_len, uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const atls_span m = msgs[i];
+  uint8_t* o = out + (size_t)i * out_len;
+  if (op == ATLS_HASH_SHA) {
+    sha_x((int)hl, data + m.off, m.len, o);
+    return;
+  }
+  const atls_span k = keys[i];
+  if (op == ATLS_HASH_HKDF_EXPAND) {
+    hkdf_expand((int)hl, data + k.off, k.len, data + m.off, m.len, o, out_len);
+    return;
+  }
+  // HMAC(key, msg); HKDF-Extract(salt, ikm) = HMAC(salt, ikm) (hash/hkdf.rs:24-32)
+  hmac_parts((int)hl, data + k.off, k.len, data + m.off, m.len, nullptr, 0, nullptr, 0, o);
+}
+
+// KeySchedule::do_key_schedule (net/key_schedule.rs:170-222) from the (EC)DHE shared secret and
+// the ClientHello..ServerHello transcript hash, then the application traffic secrets
+// (WriteKeys::application_keys_from_master_secret, :87-114) from the ..server Finished hash. One
+// thread per connection; out = {c hs, s hs, master, c ap, s ap} traffic secrets, HashLen each.
+__global__ void key_schedule_kernel(uint32_t hl, const uint8_t* __restrict__ shared, uint32_t shared_len,
+                                    const uint8_t* __restrict__ hello, const uint8_t* __restrict__ fin, uint32_t n,
+                                    uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int h = (int)hl;
+  uint8_t zeros[48], empty_hash[48], early[48], derived[48], hs[48];
+  for (int j = 0; j < 48; j++) zeros[j] = 0;
+  sha_x(h, zeros, 0, empty_hash);
+  uint8_t* o = out + (size_t)i * 5 * hl;
+  hmac_parts(h, zeros, hl, zeros, hl, nullptr, 0, nullptr, 0, early);                 // Early Secret
+  expand_label(h, early, "derived", 7, empty_hash, hl, hl, derived);
+  hmac_parts(h, derived, hl, shared + (size_t)i * shared_len, shared_len, nullptr, 0, nullptr, 0, hs);  // Handshake
+  const uint8_t* hh = hello + (size_t)i * hl;
+  expand_label(h, hs, "c hs traffic", 12, hh, hl, hl, o);
+  expand_label(h, hs, "s hs traffic", 12, hh, hl, hl, o + hl);
+  expand_label(h, hs, "derived", 7, empty_hash, hl, hl, derived);
+  hmac_parts(h, derived, hl, zeros, hl, nullptr, 0, nullptr, 0, o + 2 * hl);          // Master Secret
+  if (fin) {
+    const uint8_t* fh = fin + (size_t)i * hl;
+    expand_label(h, o + 2 * hl, "c ap traffic", 12, fh, hl, hl, o + 3 * hl);
+    expand_label(h, o + 2 * hl, "s ap traffic", 12, fh, hl, hl, o + 4 * hl);
+  }
+}
+
 }  // namespace atls
+
+extern "C" int atls_launch_hash(int op, uint32_t hl, const uint8_t* data, const atls_span* keys, const atls_span* msgs,
+                                uint32_t n, uint32_t out_len, uint8_t* out, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(atls::hash_kernel, dim3((n + 63) / 64), dim3(64), 0, s, op, hl, data, keys, msgs, n, out_len, out);
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}
+
+extern "C" int atls_launch_key_schedule(uint32_t hl, const uint8_t* shared, uint32_t shared_len, const uint8_t* hello,
+                                        const uint8_t* fin, uint32_t n, uint8_t* out, hipStream_t s) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(atls::key_schedule_kernel, dim3((n + 63) / 64), dim3(64), 0, s, hl, shared, shared_len, hello, fin,
+                     n, out);
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}
 
 extern "C" int atls_launch_derive(uint16_t suite, const uint8_t* secrets, uint32_t secret_len, uint32_t n,
                                   atls_key* out, hipStream_t s) {

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/atls.h"
+#include "record_split.h"
 
 namespace {
 
@@ -35,7 +36,6 @@ constexpr size_t kMaxFragment = size_t(1) << 14;  // RFC 8446 §5.1
 constexpr int kUnexpectedMessage = 10;            // TlsError::UnexpectedMessage, alert.rs:22
 constexpr int kBrokenPipe = 254;                  // TlsError::BrokenPipe, alert.rs:44
 
-bool record_type_ok(uint32_t b) { return b == 0 || (b >= 20 && b <= 23); }  // RecordType::new, record.rs:23-32
 
 // Grow-only page-locked host buffer: the engine's copies from it run at full PCIe speed.
 struct Pinned {
@@ -87,22 +87,9 @@ bool send_all(int fd, const uint8_t* p, size_t n) {
   return true;
 }
 
-// Moves the whole records at the front of c.rx to c.wire with Record::from_raw's checks.
+// Moves the whole records at the front of c.rx to c.wire (record_split.h, Record::from_raw checks).
 void split(Conn& c) {
-  size_t pos = 0;
-  const size_t end = c.rx.size();
-  while (end - pos >= 5) {
-    const uint8_t* h = c.rx.data() + pos;
-    const size_t len = ((size_t)h[3] << 8) | h[4];
-    if (end - pos < 5 + len) break;  // partial record
-    if (!record_type_ok(h[0]) || len < 16) {  // not a RecordType / shorter than a tag (record.rs:208)
-      c.err = ATLS_DECODE_ERROR;
-      break;
-    }
-    c.offs.push_back((uint32_t)c.wire.size());
-    c.wire.insert(c.wire.end(), h, h + 5 + len);
-    pos += 5 + len;
-  }
+  const size_t pos = atls_split::split_records(c.rx.data(), c.rx.size(), c.wire, c.offs, c.err);
   c.rx.erase(c.rx.begin(), c.rx.begin() + (std::ptrdiff_t)pos);
 }
 
@@ -128,7 +115,18 @@ int install_keys(atls_stream_batch* sb) {
   return rc;
 }
 
-bool valid_conn(atls_stream_batch* sb, int conn) { return sb && conn >= 0 && (size_t)conn < sb->conns.size(); }
+// Connection ids are checked under sb->mu: atls_sb_add_connection may grow the vector meanwhile.
+bool valid_conn_locked(atls_stream_batch* sb, int conn) { return conn >= 0 && (size_t)conn < sb->conns.size(); }
+
+// A connection's keys as the engine would accept them (engine.cpp key_status, plus the 12-byte
+// static IV of Key::from_hkdf, key_schedule.rs:44): rejected at add time, so one bad key cannot
+// make every later flush of the batch fail.
+int key_check(const atls_key& k) {
+  if (k.suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) return (k.key_len == 32 && k.iv_len == 12) ? ATLS_OK : ATLS_ILLEGAL_PARAMETER;
+  if (k.suite == ATLS_TLS_AES_128_GCM_SHA256 || k.suite == ATLS_TLS_AES_256_GCM_SHA384)
+    return ((k.key_len == 16 || k.key_len == 24 || k.key_len == 32) && k.iv_len == 12) ? ATLS_OK : ATLS_ILLEGAL_PARAMETER;
+  return ATLS_INSUFFICIENT_SECURITY;
+}
 
 }  // namespace
 
@@ -145,6 +143,8 @@ void atls_sb_destroy(atls_stream_batch* sb) { delete sb; }
 
 int atls_sb_add_connection(atls_stream_batch* sb, int fd, const atls_key* write_key, const atls_key* read_key) {
   if (!sb || !write_key || !read_key) return -ATLS_ILLEGAL_PARAMETER;
+  if (const int rc = key_check(*write_key)) return -rc;
+  if (const int rc = key_check(*read_key)) return -rc;
   std::lock_guard<std::mutex> lk(sb->mu);
   Conn c;
   c.fd = fd;
@@ -158,9 +158,10 @@ int atls_sb_add_connection(atls_stream_batch* sb, int fd, const atls_key* write_
 }
 
 int atls_sb_write(atls_stream_batch* sb, int conn, uint8_t content_type, const uint8_t* data, size_t len) {
-  if (!valid_conn(sb, conn) || (len && !data) || content_type == 0 || !record_type_ok(content_type))
+  if (!sb || (len && !data) || content_type == 0 || !atls_split::record_type_ok(content_type))
     return ATLS_ILLEGAL_PARAMETER;
   std::lock_guard<std::mutex> lk(sb->mu);
+  if (!valid_conn_locked(sb, conn)) return ATLS_ILLEGAL_PARAMETER;
   Conn& c = sb->conns[(size_t)conn];
   if (c.err) return c.err;
   if (len == 0) c.out.push_back(Record{content_type, {}});
@@ -220,8 +221,9 @@ long atls_sb_flush(atls_stream_batch* sb) {
 }
 
 int atls_sb_feed(atls_stream_batch* sb, int conn, const uint8_t* data, size_t len) {
-  if (!valid_conn(sb, conn) || (len && !data)) return ATLS_ILLEGAL_PARAMETER;
+  if (!sb || (len && !data)) return ATLS_ILLEGAL_PARAMETER;
   std::lock_guard<std::mutex> lk(sb->mu);
+  if (!valid_conn_locked(sb, conn)) return ATLS_ILLEGAL_PARAMETER;
   Conn& c = sb->conns[(size_t)conn];
   c.rx.insert(c.rx.end(), data, data + len);
   if (!c.err) split(c);
@@ -229,10 +231,11 @@ int atls_sb_feed(atls_stream_batch* sb, int conn, const uint8_t* data, size_t le
 }
 
 long atls_sb_recv(atls_stream_batch* sb, int conn, size_t max_bytes) {
-  if (!valid_conn(sb, conn) || max_bytes == 0) return -ATLS_ILLEGAL_PARAMETER;
+  if (!sb || max_bytes == 0) return -ATLS_ILLEGAL_PARAMETER;
   int fd;
   {
     std::lock_guard<std::mutex> lk(sb->mu);
+    if (!valid_conn_locked(sb, conn)) return -ATLS_ILLEGAL_PARAMETER;
     fd = sb->conns[(size_t)conn].fd;
   }
   thread_local std::vector<uint8_t> buf;  // reused: a fresh vector would zero max_bytes per call
@@ -304,11 +307,12 @@ long atls_sb_open_pending(atls_stream_batch* sb) {
 }
 
 int atls_sb_read(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size_t* out_len) {
-  if (!valid_conn(sb, conn) || !out_len || (cap && !buf)) return ATLS_ILLEGAL_PARAMETER;
+  if (!sb || !out_len || (cap && !buf)) return ATLS_ILLEGAL_PARAMETER;
   for (;;) {
     bool pending;
     {
       std::lock_guard<std::mutex> lk(sb->mu);
+      if (!valid_conn_locked(sb, conn)) return ATLS_ILLEGAL_PARAMETER;
       Conn& c = sb->conns[(size_t)conn];
       if (!c.inbox.empty()) {
         Record& r = c.inbox.front();

@@ -161,6 +161,33 @@ int atls_open_batch(atls_engine* e, const atls_rec* recs, uint32_t n, const void
 int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, size_t secret_len, uint32_t n,
                      atls_key* out_keys);
 
+/* ---- Hashes on the device (hash/sha256.rs .. hkdf.rs; per connection, not per record) ------------------------
+ * One batch item per message: item i reads data + msg[i].off (msg[i].len bytes) and, for the keyed
+ * ops, data + key[i].off; its output goes to out + i * out_len. hash_len 32 = SHA-256, 48 = SHA-384.
+ *   ATLS_HASH_SHA           sha256 / sha384 (hash/sha256.rs:188-192, sha384.rs:202-206); out_len = hash_len
+ *   ATLS_HASH_HMAC          Hmac::new(hash, key).update(msg).result() (hash/hmac.rs:29-78); keys longer
+ *                           than 64 bytes are hashed first for both hashes, as the reference does
+ *   ATLS_HASH_HKDF_EXTRACT  Hkdf::extract(hash, salt = key, ikm = msg) (hash/hkdf.rs:24-32)
+ *   ATLS_HASH_HKDF_EXPAND   Hkdf::expand(info = msg, out_len) with PRK = key (hash/hkdf.rs:35-65);
+ *                           out_len > 255 * hash_len is ATLS_ILLEGAL_PARAMETER (the reference's None)
+ * data / key / msg / out are host memory. */
+typedef struct {
+  uint64_t off;
+  uint32_t len;
+  uint32_t reserved;
+} atls_span;
+enum { ATLS_HASH_SHA = 0, ATLS_HASH_HMAC = 1, ATLS_HASH_HKDF_EXTRACT = 2, ATLS_HASH_HKDF_EXPAND = 3 };
+int atls_hash_batch(atls_engine* e, int op, uint32_t hash_len, const uint8_t* data, size_t data_len,
+                    const atls_span* keys, const atls_span* msgs, uint32_t n, uint32_t out_len, uint8_t* out);
+/* The TLS 1.3 secret chain of n connections (KeySchedule::do_key_schedule, net/key_schedule.rs:170-222,
+ * then WriteKeys::application_keys_from_master_secret, :87-114): from each (EC)DHE shared secret
+ * (shared_len bytes) and ClientHello..ServerHello transcript hash (hash_len), out receives per
+ * connection 5 secrets of hash_len bytes: client / server handshake traffic secret, master secret,
+ * client / server application traffic secret 0 (from the ..server Finished transcript hash in
+ * handshake_hashes; NULL leaves those two zero). Feed the traffic secrets to atls_derive_keys. */
+int atls_key_schedule(atls_engine* e, uint32_t hash_len, const uint8_t* shared, size_t shared_len,
+                      const uint8_t* hello_hashes, const uint8_t* handshake_hashes, uint32_t n, uint8_t* out);
+
 /* The AES block cipher, AES::init + AES::encrypt / AES::decrypt (crypto/aes/cipher.rs:167-215),
  * over nblocks independent 16-byte blocks (ECB) under key slot key_slot of the engine's table
  * (an AES suite slot; otherwise ATLS_ILLEGAL_PARAMETER). Not on the record path -- GCM only

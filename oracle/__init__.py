@@ -211,6 +211,18 @@ def key_from_secret(hash_len, secret, key_len, iv_len=12):
     return rc, bytes(k)[:key_len], bytes(v)[:iv_len]
 
 
+def key_schedule(hash_len, shared, hello_hash, handshake_hash=None):
+    """key_schedule.rs:170-222 + :87-114 -> (c_hs, s_hs, master, c_ap, s_ap) secrets."""
+    s, sl = _buf(shared)
+    h, _ = _buf(hello_hash)
+    f = _buf(handshake_hash)[0] if handshake_hash is not None else None
+    o = _out(5 * hash_len)
+    rc = lib().ora_key_schedule(hash_len, s, ctypes.c_size_t(sl), h, f, o)
+    assert rc == 0
+    b = bytes(o)
+    return tuple(b[i * hash_len:(i + 1) * hash_len] for i in range(5 if handshake_hash is not None else 3))
+
+
 def per_record_nonce(iv, seq):
     v, _ = _buf(iv)
     o = _out(12)

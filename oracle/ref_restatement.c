@@ -733,7 +733,7 @@ size_t ora_hkdf_expand_label(const uint8_t* label, size_t label_len, const uint8
   memcpy(buf + p, label, label_len);
   p += label_len;
   buf[p++] = (uint8_t)ctx_len;
-  memcpy(buf + p, ctx, ctx_len);
+  if (ctx_len) memcpy(buf + p, ctx, ctx_len); /* ctx may be NULL when empty (memcpy UB, UBSan) */
   return p + ctx_len;
 }
 /* net/key_schedule.rs:40-50 Key::from_hkdf (traffic secret is the PRK). */
@@ -744,6 +744,35 @@ int ora_key_from_secret(int hash, const uint8_t* secret, size_t secret_len, size
   if (ora_hkdf_expand(hash, secret, secret_len, info, il, key, key_len)) return ORA_INTERNAL_ERROR;
   il = ora_hkdf_expand_label((const uint8_t*)"iv", 2, NULL, 0, iv_len, info);
   if (ora_hkdf_expand(hash, secret, secret_len, info, il, iv, iv_len)) return ORA_INTERNAL_ERROR;
+  return ORA_OK;
+}
+/* net/key_schedule.rs:170-222 KeySchedule::do_key_schedule (after the X25519 shared secret) and
+ * :87-114 WriteKeys::application_keys_from_master_secret. out = 5 secrets of HashLen bytes:
+ * client / server handshake traffic secret, master secret (the PRK), client / server application
+ * traffic secret 0. handshake_hash may be NULL (the last two are then left untouched). */
+int ora_key_schedule(int hash, const uint8_t* shared, size_t shared_len, const uint8_t* hello_hash,
+                     const uint8_t* handshake_hash, uint8_t* out) {
+  const size_t hl = (size_t)hash;
+  uint8_t zeros[48], empty_hash[48], early[48], derived[48], hs[48], info[300];
+  memset(zeros, 0, sizeof zeros);
+  sha_x(hash, (const uint8_t*)"", 0, empty_hash);
+  ora_hkdf_extract(hash, zeros, hl, zeros, hl, early);                 /* Early Secret */
+  size_t il = ora_hkdf_expand_label((const uint8_t*)"derived", 7, empty_hash, hl, hl, info);
+  if (ora_hkdf_expand(hash, early, hl, info, il, derived, hl)) return ORA_INTERNAL_ERROR;
+  ora_hkdf_extract(hash, derived, hl, shared, shared_len, hs);         /* Handshake Secret */
+  il = ora_hkdf_expand_label((const uint8_t*)"c hs traffic", 12, hello_hash, hl, hl, info);
+  if (ora_hkdf_expand(hash, hs, hl, info, il, out, hl)) return ORA_INTERNAL_ERROR;
+  il = ora_hkdf_expand_label((const uint8_t*)"s hs traffic", 12, hello_hash, hl, hl, info);
+  if (ora_hkdf_expand(hash, hs, hl, info, il, out + hl, hl)) return ORA_INTERNAL_ERROR;
+  il = ora_hkdf_expand_label((const uint8_t*)"derived", 7, empty_hash, hl, hl, info);
+  if (ora_hkdf_expand(hash, hs, hl, info, il, derived, hl)) return ORA_INTERNAL_ERROR;
+  ora_hkdf_extract(hash, derived, hl, zeros, hl, out + 2 * hl);        /* Master Secret */
+  if (handshake_hash) {
+    il = ora_hkdf_expand_label((const uint8_t*)"c ap traffic", 12, handshake_hash, hl, hl, info);
+    if (ora_hkdf_expand(hash, out + 2 * hl, hl, info, il, out + 3 * hl, hl)) return ORA_INTERNAL_ERROR;
+    il = ora_hkdf_expand_label((const uint8_t*)"s ap traffic", 12, handshake_hash, hl, hl, info);
+    if (ora_hkdf_expand(hash, out + 2 * hl, hl, info, il, out + 4 * hl, hl)) return ORA_INTERNAL_ERROR;
+  }
   return ORA_OK;
 }
 /* net/key_schedule.rs:51-64 */

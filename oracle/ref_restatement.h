@@ -85,6 +85,8 @@ size_t ora_hkdf_expand_label(const uint8_t* label, size_t label_len, const uint8
                              size_t out_len, uint8_t* buf);
 int ora_key_from_secret(int hash, const uint8_t* secret, size_t secret_len, size_t key_len, size_t iv_len,
                         uint8_t* key, uint8_t* iv);
+int ora_key_schedule(int hash, const uint8_t* shared, size_t shared_len, const uint8_t* hello_hash,
+                     const uint8_t* handshake_hash, uint8_t* out);
 void ora_per_record_nonce(const uint8_t iv[12], uint64_t seq, uint8_t out[12]);
 
 /* net/record.rs: RecordPayloadProtection::encrypt / decrypt for one record */
