@@ -30,11 +30,13 @@ namespace atls {
 #endif
 #ifndef ATLS_DBG_SKIP
 #define ATLS_DBG_SKIP 0  // timing experiments only (wrong results): 1 lane combine, 2 general steps, 4 GHASH
-                         // table, 8 GHASH multiply in general steps, 16 last step, 32 first step
+                         // table, 8 GHASH multiply in general steps, 16 last step, 32 first step,
+                         // 64 the last AES round's lookups
 #endif
 #ifndef ATLS_CTR_CACHE
 #define ATLS_CTR_CACHE 1
 #endif
+
 #ifndef ATLS_DBG_SHARED_GHASH
 #define ATLS_DBG_SHARED_GHASH 0  // timing experiment only (wrong tags): one GHASH table per workgroup,
                                  // 16 waves per CU, to price the residency a per-key table would buy
@@ -103,7 +105,12 @@ __device__ __forceinline__ void aes_rounds_tt(uint32_t (&s)[4], const uint32_t* 
                                               uint32_t lb) {
 #pragma unroll
   for (int r = R0; r < NR; r++) tt_round(s, rkr + 4 * r, lb);
-  tt_final(s, rk + 4 * NR, lb);
+  if (ATLS_DBG_SKIP & 64) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[c] ^= rk[4 * NR + c];
+  } else {
+    tt_final(s, rk + 4 * NR, lb);
+  }
 }
 
 template <int NR>
@@ -303,6 +310,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   if (lane == 0) { if (m >= 64) s_last = (int64_t)(m / 64) * 64; }
   else if ((uint32_t)lane <= m) s_last = (int64_t)lane + (int64_t)((m - (uint32_t)lane) / 64) * 64;
   const uint32_t e_comb = s_last >= 1 ? S - (uint32_t)s_last : 1u;  // 1..64
+  // the lane's combine multiplier H^e_comb, loaded now so its latency hides under the steps
+  uint32_t hp[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e_comb - 1][w];
 
   TT_STAMP(t_setup);
   for (uint32_t base = 0; base < S; base += 64) {
@@ -444,9 +455,6 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   // ---- lane combine: Z = sum_l Y_l * H^(S - s_last(l)) ----
   uint32_t z[4] = {0, 0, 0, 0};
   if (s_last >= 1) {
-    uint32_t hp[4];
-#pragma unroll
-    for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e_comb - 1][w];
     const uint32_t yb[4] = {bswap32(y[0]), bswap32(y[1]), bswap32(y[2]), bswap32(y[3])};
     gf_mul_comb(yb, hp, z);
   }
