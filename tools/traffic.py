@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {"c2": "c2_aes128gcm_64Ki_x_16KiB", "c3": "c3_chacha20poly1305_64Ki_x_1.5KiB",
-           "c4": "c4_aes256gcm_1Mi_x_16KiB"}
+           "c4": "c4_aes256gcm_1Mi_x_16KiB", "c5": "c5_mixed_256Ki_x_64B-16KiB"}
 
 
 def per_kernel(path, counter):
@@ -29,13 +29,15 @@ def per_kernel(path, counter):
 def main():
     from anothertls_amd import workload
 
-    d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r01")
+    d = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "profiles", "r02")
     out = {"_about": "HBM traffic per launch of the dominant kernel from rocprofv3 PMC passes (separate --pmc "
-                     "FETCH_SIZE / WRITE_SIZE runs of `bench.py --config <cfg> --steps 5 --warmup 1`, "
-                     "tools/profile_round.sh; CSVs in profiles/r01/, reduced by tools/traffic.py). FETCH_SIZE is "
+                     "FETCH_SIZE / WRITE_SIZE runs of `bench.py --config <cfg> --steps 20 --warmup 3`, "
+                     "tools/profile_round.sh; CSVs in profiles/r02/, reduced by tools/traffic.py). FETCH_SIZE is "
                      "doubled (gfx950 reports 1/2 of wide streaming reads, MI355X_MICROARCH.md §HBM), WRITE_SIZE as "
                      "reported. Averaged over the kernel's dispatches. Units: bytes."}
     for tag, cfg in CONFIGS.items():
+        if not os.path.exists(os.path.join(d, f"{tag}_pmc_fetch.csv")):
+            continue
         f = per_kernel(os.path.join(d, f"{tag}_pmc_fetch.csv"), "FETCH_SIZE")
         w = per_kernel(os.path.join(d, f"{tag}_pmc_write.csv"), "WRITE_SIZE")
         rec = [n for n in f if "atls::gcm_kernel" in n or "atls::chacha_kernel" in n]
@@ -44,6 +46,10 @@ def main():
         write = sum(w[k]) / len(w[k])
         b = workload.shard_batch(cfg, 0)
         alg = 2 * b["payload"] + 16 * len(b["recs"])
+        if tag == "c5":  # planned batch: the AES-GCM kernel handles the AES records only
+            suites = b["keys"]["suite"][b["recs"]["key_slot"]]
+            aes = suites != 0x1303
+            alg = int(2 * (b["recs"]["len"][aes].astype("int64") + 1).sum() + 16 * aes.sum())
         out[cfg] = {"kernel": k, "fetch_bytes": round(fetch), "write_bytes": round(write),
                     "hbm_bytes_per_launch": round(fetch + write), "algorithmic_bytes_per_launch": alg,
                     "ratio": round((fetch + write) / alg, 4)}
