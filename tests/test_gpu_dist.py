@@ -150,3 +150,60 @@ def test_two_rank_seal_sharded_with_engine():
     got_out, got_tags = res[0][2]
     assert got_tags == ref_tags.tobytes()
     assert got_out == ref_out.tobytes()
+
+
+def test_multi_engine_edge_cases_raw_records_and_wire_open():
+    rng = np.random.default_rng(12)
+    # RAW records (explicit nonce || AAD in aux) of mixed suites and random lengths
+    n = 40
+    lens = rng.integers(0, 5000, n).astype(np.uint64)
+    b = workload.tls_batch(n, lens, lambda k: np.array([0x1301, 0x1303, 0x1302] * k, np.uint16)[:k], n_keys=3)
+    recs = b["recs"].copy()
+    recs["mode"] = atls.MODE_RAW
+    recs["iv_len"] = 12
+    recs["aad_len"] = rng.integers(0, 30, n)
+    recs["aux_off"] = np.arange(n, dtype=np.uint64) * 64
+    aux = rng.integers(0, 256, 64 * n + 16, dtype=np.uint8)
+    inbuf = rng.integers(0, 256, b["in_bytes"] + 16, dtype=np.uint8)
+    e = atls.Engine(0)
+    e.set_keys(b["keys"])
+    ref_out = np.zeros(b["out_bytes"] + 16, np.uint8)
+    ref_tags = np.zeros(16 * n, np.uint8)
+    e.seal_batch(recs, inbuf, aux, ref_out, ref_tags)
+    m = atls.MultiEngine([0, 0, 0])
+    m.set_keys(b["keys"])
+    dev = torch.device("cuda", 0)
+    d_in, d_aux = torch.from_numpy(inbuf).to(dev), torch.from_numpy(aux).to(dev)
+    d_out = torch.zeros(b["out_bytes"] + 16, dtype=torch.uint8, device=dev)
+    d_tags = torch.zeros(16 * n, dtype=torch.uint8, device=dev)
+    m.seal_batch(recs, d_in, d_aux, d_out, d_tags, flags=atls.FLAG_DEVICE_PTRS)
+    assert np.array_equal(d_tags.cpu().numpy(), ref_tags) and np.array_equal(d_out.cpu().numpy(), ref_out)
+    m.close()
+    # more parts than records: empty parts are skipped
+    m = atls.MultiEngine([0] * 5)
+    m.set_keys(b["keys"])
+    few = b["recs"][:3]
+    out = np.zeros(b["out_bytes"] + 16, np.uint8)
+    tags = np.zeros(48, np.uint8)
+    m.seal_batch(few, inbuf, np.zeros(16, np.uint8), out, tags)
+    o2, t2 = np.zeros_like(out), np.zeros_like(tags)
+    e.seal_batch(few, inbuf, np.zeros(16, np.uint8), o2, t2)
+    assert np.array_equal(out, o2) and np.array_equal(tags, t2)
+    # WIRE records: seal through one engine, open through the multi engine (device buffers)
+    wb = workload.wire_batch(b)
+    wire = np.zeros(wb["out_bytes"] + 16, np.uint8)
+    e.seal_batch(wb["recs"], inbuf, np.zeros(16, np.uint8), wire, np.zeros(16 * n, np.uint8))
+    orecs, pt_bytes = workload.wire_open_descs(wb["recs"])
+    d_wire = torch.from_numpy(wire).to(dev)
+    d_pt = torch.zeros(pt_bytes + 16, dtype=torch.uint8, device=dev)
+    d_res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
+    m.open_batch(orecs, d_wire, torch.zeros(16, dtype=torch.uint8, device=dev), None, d_pt, d_res,
+                 flags=atls.FLAG_DEVICE_PTRS)
+    res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
+    assert (res["status"] == 0).all() and (res["content_len"] == lens).all()
+    pt = d_pt.cpu().numpy()
+    for i in range(n):
+        o, s, L = int(orecs[i]["out_off"]), int(b["recs"][i]["in_off"]), int(lens[i])
+        assert pt[o:o + L].tobytes() == inbuf[s:s + L].tobytes(), i
+    m.close()
+    e.close()
