@@ -423,8 +423,16 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 // of 32 (C3: 690 -> 906 GiB/s). Direct batches launch both kernels after batch_prep (plan.hip)
 // has recorded the longest record; each kernel reads it and only the matching one does the work.
 // Planned batches (mixed lengths) launch G = 16 only.
+// Minimum waves per SIMD of the seal / open kernels (__launch_bounds__): caps their VGPRs
+// (3 -> 168, 4 -> 128), i.e. how many waves of each a SIMD holds.
+#ifndef ATLS_CHACHA_MINW_SEAL
+#define ATLS_CHACHA_MINW_SEAL 1
+#endif
+#ifndef ATLS_CHACHA_MINW_OPEN
+#define ATLS_CHACHA_MINW_OPEN 3  // 169 -> 168 VGPRs: 3 open waves per SIMD instead of 2 (C3 open 0.113 -> 0.106 ms)
+#endif
 template <bool OPEN, int G>
-__global__ __launch_bounds__(256) void chacha_kernel(ChArgs A) {
+__global__ __launch_bounds__(256, OPEN ? ATLS_CHACHA_MINW_OPEN : ATLS_CHACHA_MINW_SEAL) void chacha_kernel(ChArgs A) {
   const int lane = threadIdx.x & 63;
   if (A.wgmax) {
     uint32_t mx = 0;
