@@ -134,8 +134,6 @@ struct ChArgs {
   PlanHdr* plan;
   uint32_t* err;        // direct mode: sticky error word
   uint32_t n_slots;     // direct mode: key-table size
-  const uint32_t* wgmax;  // direct mode: per-workgroup longest record (batch_prep), or nullptr
-  uint32_t n_wgmax;
 };
 
 template <bool OPEN, int G>
@@ -420,9 +418,13 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 // G = 4 (batches whose records are all short, ATLS_CHACHA_SHORT): 16 positions per wave and step,
 // one per 4-lane group: the per-record Poly1305 set-up (r powers, lane scan, combine) is shared
 // by 4 lanes instead of 16, and a 1.5 KiB record's 26 ChaCha blocks fill 28 lane-slots instead
-// of 32 (C3: 690 -> 906 GiB/s). Direct batches launch both kernels after batch_prep (plan.hip)
-// has recorded the longest record; each kernel reads it and only the matching one does the work.
-// Planned batches (mixed lengths) launch G = 16 only.
+// of 32 (C3: 690 -> 906 GiB/s). Direct batches: a wave takes 16 consecutive positions per step
+// and picks the width from their longest record -- 4 lanes each if all are short, else 16 lanes
+// in four rounds of 4 records -- so no pass over the batch precedes the launch (an earlier version ran a
+// batch_prep kernel for the batch's longest record and launched one kernel per width: two extra
+// dispatches, ≈10 µs of every C3 batch). Planned batches (mixed lengths, longest first) run
+// G = 16, 4 positions per wave and step, keeping the fine round-robin the longest-first order
+// needs for balance.
 // Minimum waves per SIMD of the seal / open kernels (__launch_bounds__): caps their VGPRs
 // (3 -> 168, 4 -> 128), i.e. how many waves of each a SIMD holds.
 #ifndef ATLS_CHACHA_MINW_SEAL
@@ -432,15 +434,7 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 #define ATLS_CHACHA_MINW_OPEN 3  // 169 -> 168 VGPRs: 3 open waves per SIMD instead of 2 (C3 open 0.113 -> 0.106 ms)
 #endif
 template <bool OPEN, int G>
-__global__ __launch_bounds__(256, OPEN ? ATLS_CHACHA_MINW_OPEN : ATLS_CHACHA_MINW_SEAL) void chacha_kernel(ChArgs A) {
-  const int lane = threadIdx.x & 63;
-  if (A.wgmax) {
-    uint32_t mx = 0;
-    for (uint32_t i = (uint32_t)lane; i < A.n_wgmax; i += 64) mx = max(mx, A.wgmax[i]);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
-    if ((mx <= (uint32_t)ATLS_CHACHA_SHORT) != (G == 4)) return;  // the other kernel's batch
-  }
+__device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
   const WorkList W{A.idx, A.plan, kListChacha, A.n};
   const uint32_t cnt = W.size();
   constexpr uint32_t kPer = 64u / G;
@@ -450,26 +444,49 @@ __global__ __launch_bounds__(256, OPEN ? ATLS_CHACHA_MINW_OPEN : ATLS_CHACHA_MIN
     chacha_group<OPEN, G>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
 }
 
+// Direct batch: 16 positions per wave and step, the width chosen per step from their longest record.
+template <bool OPEN>
+__device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
+  const WorkList W{nullptr, nullptr, kListChacha, A.n};
+  const uint32_t cnt = A.n;
+  const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
+  const uint32_t stride = gridDim.x * blockDim.x / 64u * 16u;
+  for (uint32_t q0 = wave * 16u; q0 < cnt; q0 += stride) {
+    uint32_t mx = (lane < 16 && q0 + (uint32_t)lane < cnt) ? A.recs[q0 + (uint32_t)lane].len : 0u;
+#pragma unroll
+    for (int off = 8; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
+    if (mx <= (uint32_t)ATLS_CHACHA_SHORT) {
+      chacha_group<OPEN, 4>(A, W, q0 + (uint32_t)lane / 4u, cnt, lane & 3);
+    } else {
+#pragma unroll 1
+      for (uint32_t rr = 0; rr < 4u; rr++) chacha_group<OPEN, 16>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15);
+    }
+  }
+}
+
+template <bool OPEN>
+__global__ __launch_bounds__(256, OPEN ? ATLS_CHACHA_MINW_OPEN : ATLS_CHACHA_MINW_SEAL) void chacha_kernel(ChArgs A) {
+  const int lane = threadIdx.x & 63;
+  if (A.idx) chacha_batch<OPEN, 16>(A, lane);
+  else chacha_direct<OPEN>(A, lane);
+}
+
 }  // namespace atls
 
-// wgmax / n_wgmax: batch_prep's per-workgroup longest record for a direct batch (both kernel
-// widths are launched, the matching one works), nullptr for a planned batch (G = 16 only).
+// idx / plan: the batch plan's work lists (G = 16), or nullptr for a direct batch (per-step widths).
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
-                                  uint32_t n_slots, const uint32_t* wgmax, uint32_t n_wgmax, int grid, hipStream_t s) {
+                                  uint32_t n_slots, int grid, hipStream_t s) {
   if (n == 0) return 0;
   atls::ChArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, idx,
-                 (atls::PlanHdr*)plan, err, n_slots, wgmax, n_wgmax};
-  const uint32_t want16 = (n + 15u) / 16u, want4 = (n + 63u) / 64u;  // 4 waves x 4 / x 16 positions
-  const uint32_t g16 = (uint32_t)grid < want16 ? (uint32_t)grid : want16;
-  const uint32_t g4 = (uint32_t)grid < want4 ? (uint32_t)grid : want4;
-  if (open) {
-    hipLaunchKernelGGL((atls::chacha_kernel<true, 16>), dim3(g16), dim3(256), 0, s, A);
-    if (wgmax) hipLaunchKernelGGL((atls::chacha_kernel<true, 4>), dim3(g4), dim3(256), 0, s, A);
-  } else {
-    hipLaunchKernelGGL((atls::chacha_kernel<false, 16>), dim3(g16), dim3(256), 0, s, A);
-    if (wgmax) hipLaunchKernelGGL((atls::chacha_kernel<false, 4>), dim3(g4), dim3(256), 0, s, A);
-  }
+                 (atls::PlanHdr*)plan, err, n_slots};
+  // the grid of the wider need (4 waves x 4 positions per workgroup at G = 16); the G = 4 path
+  // strides over 16 positions per wave and simply finishes its list sooner
+  const uint32_t want16 = (n + 15u) / 16u;
+  const uint32_t g = (uint32_t)grid < want16 ? (uint32_t)grid : want16;
+  if (open) hipLaunchKernelGGL((atls::chacha_kernel<true>), dim3(g), dim3(256), 0, s, A);
+  else hipLaunchKernelGGL((atls::chacha_kernel<false>), dim3(g), dim3(256), 0, s, A);
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }

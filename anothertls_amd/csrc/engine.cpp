@@ -37,9 +37,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
-                                  uint32_t n_slots, const uint32_t* wgmax, uint32_t n_wgmax, int grid, hipStream_t s);
-extern "C" int atls_launch_prep(const atls_rec* recs, uint32_t n, uint32_t* err, uint32_t* wgmax, hipStream_t s,
-                                uint32_t* n_wg);
+                                  uint32_t n_slots, int grid, hipStream_t s);
 extern "C" int atls_launch_hash(int op, uint32_t hl, const uint8_t* data, const atls_span* keys, const atls_span* msgs,
                                 uint32_t n, uint32_t out_len, uint8_t* out, hipStream_t s);
 extern "C" int atls_launch_key_schedule(uint32_t hl, const uint8_t* shared, uint32_t shared_len, const uint8_t* hello,
@@ -83,7 +81,6 @@ struct atls_engine {
   int aes_nr_mask = 0;                       // bit 0/1/2: AES slots with 10/12/14 rounds
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
   DevBuf plan, plan_keys, plan_idx, plan_wg; // batch plan (plan.hip)
-  DevBuf wgmax;                              // batch_prep: per-workgroup longest record
   int chacha_wgs = 8;                        // ATLS_CHACHA_WGS: ChaCha20-Poly1305 workgroups per CU
   bool force_plan = false;                   // ATLS_FORCE_PLAN=1: plan every batch (tests)
   bool no_pipeline = false;                  // ATLS_NO_PIPELINE=1: stage host batches in one piece
@@ -94,12 +91,22 @@ namespace {
 
 bool set_dev(atls_engine* e) { return hipSetDevice(e->device) == hipSuccess; }
 
+// The sticky error word (a kernel sets it for a descriptor it refuses) collects every batch
+// since the last synchronisation; it is read here and cleared only when set, so no batch pays
+// a memset launch and a NO_SYNC batch's refusal is reported by the next atls_engine_sync.
+int take_err(atls_engine* e, uint32_t err) {
+  if (!err) return ATLS_OK;
+  const uint32_t zero = 0;
+  if (hipMemcpy(e->err.p, &zero, 4, hipMemcpyHostToDevice) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  return ATLS_ILLEGAL_PARAMETER;
+}
+
 int finish(atls_engine* e, uint32_t flags) {
   if (flags & ATLS_FLAG_NO_SYNC) return ATLS_OK;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
   uint32_t err = 0;
   if (hipMemcpy(&err, e->err.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return ATLS_INTERNAL_ERROR;
-  return err ? ATLS_ILLEGAL_PARAMETER : ATLS_OK;
+  return take_err(e, err);
 }
 
 // Bytes a record reads at in_off and writes at out_off. TLS seal: content + type byte out;
@@ -129,15 +136,11 @@ void extents(const atls_rec* recs, uint32_t n, bool open, size_t* in_end, size_t
 int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n, const uint8_t* d_in,
                    const uint8_t* d_aux, uint8_t* d_out, uint8_t* d_tags_out, const uint8_t* d_tags_in,
                    atls_open_result* d_res, hipStream_t s, int slot) {
-  // direct batches only (one record kernel in the key table); slot: which half of the wgmax
-  // scratch this launch uses (the host pipeline's two streams run chunks concurrently)
-  if (e->has_chacha) {
-    uint32_t n_wg = 0;
-    uint32_t* wgmax = (uint32_t*)e->wgmax.p + 256 * slot;
-    if (atls_launch_prep(d_recs, n, nullptr, wgmax, s, &n_wg)) return ATLS_INTERNAL_ERROR;  // err stays sticky
+  // direct batches only (one record kernel in the key table)
+  (void)slot;
+  if (e->has_chacha)
     return atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, nullptr,
-                              e->plan.p, (uint32_t*)e->err.p, e->n_slots, wgmax, n_wg, e->cus * e->chacha_wgs, s);
-  }
+                              e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s);
   return atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, nullptr, e->plan.p, (uint32_t*)e->err.p, e->n_slots,
                          e->aes_nr_mask, e->cus, s);
@@ -172,8 +175,7 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   hipEvent_t ev[2] = {e->ev_plan, e->ev_side};
   // descriptors, aux and err are in place (stream 0) before the other stream starts
   if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, st[0]) != hipSuccess) return ATLS_INTERNAL_ERROR;
-  if (hipMemsetAsync(e->err.p, 0, 4, st[0]) != hipSuccess || hipEventRecord(ev[0], st[0]) != hipSuccess ||
-      hipStreamWaitEvent(st[1], ev[0], 0) != hipSuccess)
+  if (hipEventRecord(ev[0], st[0]) != hipSuccess || hipStreamWaitEvent(st[1], ev[0], 0) != hipSuccess)
     return ATLS_INTERNAL_ERROR;
   const auto* d_recs = (const atls_rec*)e->recs.p;
   auto* d_in = (uint8_t*)e->in.p;
@@ -265,8 +267,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   if (!dev_ptrs) {
     extents(recs, n, open, &in_end, &out_end, &aux_end);
     if (!e->in.reserve(in_end + 16) || !e->out.reserve(out_end + 16) || !e->aux.reserve(aux_end + 16) ||
-        !e->tags.reserve(16 * (size_t)n) || !e->res.reserve(sizeof(atls_open_result) * (size_t)n) ||
-        !e->wgmax.reserve(4 * 512))
+        !e->tags.reserve(16 * (size_t)n) || !e->res.reserve(sizeof(atls_open_result) * (size_t)n))
       return ATLS_INTERNAL_ERROR;
     if (!planned && n > 1 && !e->no_pipeline) {
       const int rc = run_host_pipelined(e, open, recs, n, in, aux, out, tags_out, tags_in, res, in_end, out_end, aux_end);
@@ -286,17 +287,6 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     d_tags_out = (uint8_t*)e->tags.p;
     d_tags_in = (const uint8_t*)e->tags.p;
     d_res = (atls_open_result*)e->res.p;
-  }
-  // Direct ChaCha batches: batch_prep clears err and records the longest record, from which the
-  // ChaCha kernels pick their lane width (chacha.hip); everything else: a memset of err.
-  uint32_t n_wgmax = 0;
-  const bool prep = !planned && e->has_chacha;
-  if (prep) {
-    if (!e->wgmax.reserve(4 * 512) ||
-        atls_launch_prep(d_recs, n, (uint32_t*)e->err.p, (uint32_t*)e->wgmax.p, s, &n_wgmax))
-      return ATLS_INTERNAL_ERROR;
-  } else if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess) {
-    return ATLS_INTERNAL_ERROR;
   }
   int rc = 0;
   const uint32_t* idx = nullptr;
@@ -320,8 +310,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
       cs = e->stream2;
     }
     rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, idx,
-                            e->plan.p, (uint32_t*)e->err.p, e->n_slots, prep ? (const uint32_t*)e->wgmax.p : nullptr,
-                            n_wgmax, e->cus * e->chacha_wgs, cs);
+                            e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs);
     if (rc) return rc;
     if (side && hipEventRecord(e->ev_side, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
@@ -547,8 +536,7 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
   r.iv_len = (uint8_t)iv_len;
   r.aad_len = (uint16_t)aad_len;
   std::lock_guard<std::mutex> lk(e->mu);
-  if (!set_dev(e) || !e->in.reserve(total + 16) || !e->out.reserve(len + 16) || !e->wgmax.reserve(4 * 512))
-    return ATLS_INTERNAL_ERROR;
+  if (!set_dev(e) || !e->in.reserve(total + 16) || !e->out.reserve(len + 16)) return ATLS_INTERNAL_ERROR;
   uint8_t* d = (uint8_t*)e->in.p;
   hipStream_t s = e->stream;
   if (hipMemcpyAsync(d, h, res_at, hipMemcpyHostToDevice, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
@@ -560,7 +548,6 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
     return ATLS_INTERNAL_ERROR;
   uint8_t* dout = (uint8_t*)e->out.p;
   atls_open_result* dres = (atls_open_result*)(d + res_at);
-  if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
   rc = launch_records(e, open, (const atls_rec*)e->recs.p, 1, d, d + aux_at, dout, d + tag_at, d + tag_at, dres, s, 0);
   if (rc) return rc;
   if (len && hipMemcpyAsync(h + in_at, dout, len, hipMemcpyDeviceToHost, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
@@ -569,7 +556,7 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
     return ATLS_INTERNAL_ERROR;
   uint32_t err = 0;
   std::memcpy(&err, h + err_at, 4);
-  if (err) return ATLS_ILLEGAL_PARAMETER;
+  if ((rc = take_err(e, err))) return rc;
   if (!open) {
     if (len) std::memcpy(out, h + in_at, len);
     std::memcpy(tag_out, h + tag_at, 16);
@@ -615,7 +602,8 @@ atls_engine* atls_engine_create(int device) {
   if (const char* v = std::getenv("ATLS_FORCE_PLAN")) e->force_plan = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_NO_PIPELINE")) e->no_pipeline = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_CHACHA_WGS")) e->chacha_wgs = std::max(1, std::atoi(v));
-  if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
+  if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || hipMemsetAsync(e->err.p, 0, 16, e->stream) != hipSuccess ||
+      atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
       hipStreamSynchronize(e->stream) != hipSuccess) {
     atls_engine_destroy(e);
     return nullptr;
@@ -629,7 +617,7 @@ void atls_engine_destroy(atls_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   for (DevBuf* b : {&e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
-                    &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx, &e->plan_wg, &e->wgmax})
+                    &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx, &e->plan_wg})
     b->release();
   if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);
   if (e->ev_side) (void)hipEventDestroy(e->ev_side);
@@ -775,8 +763,7 @@ int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* 
     d_in = (const uint8_t*)e->in.p;
     d_out = (uint8_t*)e->out.p;
   }
-  if (hipMemsetAsync(e->err.p, 0, 4, s) != hipSuccess ||
-      atls_launch_aes_blocks(decrypt, (const atls::KeySched*)e->ks.p + key_slot, d_in, d_out, nblocks,
+  if (atls_launch_aes_blocks(decrypt, (const atls::KeySched*)e->ks.p + key_slot, d_in, d_out, nblocks,
                              (uint32_t*)e->err.p, e->cus * 8, s))
     return ATLS_INTERNAL_ERROR;
   if (!dev) {

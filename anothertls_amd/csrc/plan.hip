@@ -131,23 +131,6 @@ __global__ __launch_bounds__(256) void plan_scatter(uint32_t n, const uint8_t* k
   }
 }
 
-// Direct batches: clears the sticky error word (instead of a memset launch; err = nullptr keeps
-// it, for the host pipeline's later chunks) and records each workgroup's longest record, from
-// which the ChaCha kernels pick their lane width.
-__global__ __launch_bounds__(256) void batch_prep(const atls_rec* recs, uint32_t n, uint32_t* err, uint32_t* wgmax) {
-  __shared__ uint32_t m;
-  if (threadIdx.x == 0) {
-    m = 0;
-    if (blockIdx.x == 0 && err) *err = 0;
-  }
-  __syncthreads();
-  uint32_t mx = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) mx = max(mx, recs[i].len);
-  atomicMax(&m, mx);
-  __syncthreads();
-  if (threadIdx.x == 0) wgmax[blockIdx.x] = m;
-}
-
 }  // namespace atls
 
 // P (device, PlanHdr), keys (n bytes), idx (n words) and wg (2 x 64 x kPlanMaxWG words) are
@@ -165,16 +148,5 @@ extern "C" int atls_launch_plan(int open, const void* ks, const atls_rec* recs, 
                      (uint32_t)(open != 0), res, err, keys, wgcount);
   hipLaunchKernelGGL(atls::plan_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)wgcount, G, wgoff, hdr);
   hipLaunchKernelGGL(atls::plan_scatter, dim3(G), dim3(256), 0, s, n, (const uint8_t*)keys, (const uint32_t*)wgoff, idx);
-  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
-}
-
-// Grid of batch_prep: returns the number of workgroups (<= kPlanMaxWG), which the ChaCha launch
-// passes on as n_wgmax.
-extern "C" int atls_launch_prep(const atls_rec* recs, uint32_t n, uint32_t* err, uint32_t* wgmax, hipStream_t s,
-                                uint32_t* n_wg) {
-  const uint32_t want = (n + 255u) / 256u;
-  const uint32_t g = want ? (want < 256u ? want : 256u) : 1u;
-  hipLaunchKernelGGL(atls::batch_prep, dim3(g), dim3(256), 0, s, recs, n, err, wgmax);
-  *n_wg = g;
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }

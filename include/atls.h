@@ -80,7 +80,9 @@ enum {
   ATLS_FLAG_DEVICE_PTRS = 1u, /* in/aux/out/tags/results are device pointers (else host memory,
                                  staged through pinned buffers with async copies) */
   ATLS_FLAG_DEVICE_RECS = 2u, /* recs is a device pointer (keeps descriptors resident) */
-  ATLS_FLAG_NO_SYNC = 4u      /* return after enqueueing; call atls_engine_sync() before reading */
+  ATLS_FLAG_NO_SYNC = 4u      /* return after enqueueing; call atls_engine_sync() before reading.
+                                 A descriptor the device refuses (DEVICE_RECS) is then reported
+                                 as ATLS_ILLEGAL_PARAMETER by that atls_engine_sync. */
 };
 
 /* One connection's write key (a "key slot"). 64 bytes. suite + key + static IV as produced by

@@ -1,5 +1,7 @@
-"""GPU: the two ChaCha20-Poly1305 lane widths (chacha.hip). A direct batch whose records are all
-short (<= ATLS_CHACHA_SHORT = 4096 B) runs 4 lanes per record, any other batch 16; both are
+"""GPU: the two ChaCha20-Poly1305 lane widths (chacha.hip). In a direct batch each wave takes 16
+consecutive records and runs them 4 lanes per record when all are short (<= ATLS_CHACHA_SHORT =
+4096 B), else 16 lanes per record in four rounds (the second case below puts one long record among
+short ones, so both widths run in one launch); both are
 checked against the oracle on the lengths that exercise the per-lane Poly1305 combine and the
 reference's F4 quirk (ChaCha20::encrypt leaves the last block unencrypted when len % 64 == 0,
 crypto/chacha20/cipher.rs:99-102), sealed and reopened, with tampered tags."""

@@ -136,3 +136,37 @@ def test_plan_large_batch_many_workgroups(atls):
         assert np.array_equal(out[o:o + L], oout[o:o + L]), i
         assert np.array_equal(tags[16 * i:16 * i + 16], otags[16 * j:16 * j + 16]), i
     eng.close()
+
+
+def test_sticky_error_reported_at_sync_and_cleared(atls):
+    """A descriptor the kernel refuses (device-resident, key slot out of range) sets the engine's
+    sticky error word: a NO_SYNC batch returns 0 and the next atls_engine_sync reports
+    IllegalParameter (47) once; later batches are clean again (engine.cpp take_err)."""
+    torch = pytest.importorskip("torch")
+    from anothertls_amd import workload
+
+    for suite in (0x1301, 0x1303):  # the GCM and ChaCha kernels both refuse it
+        b = workload.tls_batch(64, 1000, suite, n_keys=4)
+        eng = atls.Engine(0)
+        eng.set_keys(b["keys"])
+        dev = torch.device("cuda", 0)
+        recs = b["recs"].copy()
+        recs["key_slot"][7] = 99
+        d_in = torch.zeros(b["in_bytes"] + 16, dtype=torch.uint8, device=dev)
+        d_out = torch.zeros(b["out_bytes"] + 16, dtype=torch.uint8, device=dev)
+        d_tags = torch.zeros(16 * 64, dtype=torch.uint8, device=dev)
+        d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+        d_bad = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
+        d_good = torch.from_numpy(b["recs"].view(np.uint8).copy()).to(dev)
+        flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS
+        eng.seal_batch(d_bad.data_ptr(), d_in, d_aux, d_out, d_tags, flags=flags | atls.FLAG_NO_SYNC, n=64)
+        with pytest.raises(atls.TlsError) as e:
+            eng.sync()
+        assert e.value.code == 47
+        eng.sync()  # cleared
+        eng.seal_batch(d_good.data_ptr(), d_in, d_aux, d_out, d_tags, flags=flags, n=64)
+        with pytest.raises(atls.TlsError) as e:
+            eng.seal_batch(d_bad.data_ptr(), d_in, d_aux, d_out, d_tags, flags=flags, n=64)
+        assert e.value.code == 47
+        eng.seal_batch(d_good.data_ptr(), d_in, d_aux, d_out, d_tags, flags=flags, n=64)
+        eng.close()
