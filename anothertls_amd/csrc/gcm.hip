@@ -499,6 +499,271 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 #endif
 }
 
+// ---- lane groups: 64/G records of one key per wave ------------------------------------------
+// Key-grouped direct batches (plan.hip atls_launch_group): a run of records that share a key slot
+// and a step count is sealed / opened by one wave, G lanes per record. The slots are those of
+// gcm_record with lane gl = lane % G owning s = gl (mod G) of its group's record; the Horner
+// multiplier is H^G (table from the key schedule's p4g seeds) and one lane combine, one table
+// build and one counter-cache build serve 64/G records. A 16 KiB record's 1,028 slots fill
+// 64.25 sixteen-lane steps instead of 16.06 wave steps plus a per-record tail, combine and table.
+#ifndef ATLS_GCM_GROUP_LANES
+#define ATLS_GCM_GROUP_LANES 16
+#endif
+constexpr int kGroupLanes = ATLS_GCM_GROUP_LANES;
+static_assert(kGroupLanes == 16 || kGroupLanes == 32, "lane groups of 16 or 32");
+
+// XOR of x over the lane's G-lane group: DPP within 16-lane rows, then rows by readlane.
+template <int G>
+__device__ __forceinline__ uint32_t group_xor(uint32_t x) {
+  x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+  x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+  x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);
+  x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);
+  if (G == 32) {
+    const uint32_t a = (uint32_t)(__builtin_amdgcn_readlane((int)x, 0) ^ __builtin_amdgcn_readlane((int)x, 16));
+    const uint32_t b = (uint32_t)(__builtin_amdgcn_readlane((int)x, 32) ^ __builtin_amdgcn_readlane((int)x, 48));
+    x = (__lane_id() < 32) ? a : b;
+  }
+  return x;
+}
+
+// Whether the records r[0..NG) form a lane group: all present and accepted, one key slot, TLS or
+// WIRE framing, the same number of G-slot steps, and few enough steps for the counter cache
+// (lane gl holds ctr >> 8 = gl). Wave-uniform.
+template <bool OPEN, int G>
+__device__ __forceinline__ bool group_ok(const GcmArgs& A, const uint32_t* pos, uint32_t ng, uint32_t& key) {
+  uint32_t steps0 = 0;
+  for (uint32_t j = 0; j < ng; j++) {
+    const uint32_t r = uni(cptr(pos)[j]);
+    if (r == kNoRecord) return false;
+    const atls_rec d = A.recs[r];
+    if (direct_reject(d, A.ks, A.n_slots, OPEN) || d.mode == ATLS_MODE_RAW) return false;
+    if (j == 0) key = d.key_slot;
+    else if (d.key_slot != key) return false;
+    const uint64_t n_aead = (uint64_t)d.len + (OPEN ? 0u : 1u);
+    const uint64_t S = (n_aead + 15u) / 16u + 3u;  // E(J0), AAD, data, length
+    if (S > (uint64_t)G * 256u) return false;
+    const uint32_t steps = (uint32_t)((S + G - 1u) / G);
+    if (j == 0) steps0 = steps;
+    else if (steps != steps0) return false;
+  }
+  return true;
+}
+
+template <int NR, bool OPEN, int G>
+__device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx, uint32_t lb, uint32_t wb, int lane) {
+  const uint32_t gl = (uint32_t)lane & (G - 1u);
+  uint32_t rk[4 * (NR + 1)], rkr[4 * (NR + 1)];
+#pragma unroll
+  for (int i = 0; i < 4 * (NR + 1); i++) {
+    rk[i] = cptr(k->rk)[i];  // one key for the whole wave
+    rkr[i] = cptr(k->rkr)[i];
+  }
+  const atls_rec d = A.recs[rec_idx];  // this lane's group's record
+  const bool wire = d.mode == ATLS_MODE_WIRE;
+  const uint32_t len = d.len;
+  const uint32_t n_aead = OPEN ? len : len + 1u;  // record.rs:172-173 inner plaintext
+  const uint8_t* rec_in = A.in + d.in_off;
+  const uint8_t* src = rec_in + ((OPEN && wire) ? 5u : 0u);
+  uint8_t* dst = A.out + d.out_off + ((!OPEN && wire) ? 5u : 0u);
+  const bool src_al = ((reinterpret_cast<uintptr_t>(src)) & 15u) == 0;
+  const bool dst_al = ((reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+  // nonce = iv ^ (0^4 || be64(seq)) as raw words (key_schedule.rs:51-64); J0 = nonce || 1
+  const uint64_t seq = d.seq;
+  const uint32_t nraw[3] = {k->siv[0], k->siv[1] ^ bswap32((uint32_t)(seq >> 32)), k->siv[2] ^ bswap32((uint32_t)seq)};
+  uint32_t hdr0, hdr1;
+  bool hdr_ok = true;
+  if (OPEN && wire) {
+    hdr_ok = wire_header(rec_in, len, hdr0, hdr1);  // record.rs:219
+  } else {
+    const uint32_t L = n_aead + 16u;  // record.rs:176-183
+    hdr0 = 0x17u | (0x03u << 8) | (0x03u << 16) | (((L >> 8) & 0xffu) << 24);
+    hdr1 = L & 0xffu;
+  }
+  const uint32_t nb = (n_aead + 15u) / 16u;
+  const uint32_t m = nb + 2u;  // GHASH blocks: AAD, data, length
+  const uint32_t S = m + 1u;   // slots
+  const uint32_t steps = uni((S + G - 1u) / G);  // the same for every group (group_ok)
+  const uint32_t fast_end = 2u + min(len, n_aead) / 16u;  // slots [G, fast_end): whole 16-B data blocks
+
+  if (steps > 1u) {
+    uint32_t seed[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) seed[w] = k->p4g_be[G == 16 ? 0 : 1][lane >> 1][w];
+    ghash_table_entries<8>(wb, seed, lane >> 1, (lane & 1) * 8);
+    wave_lds_sync();
+  }
+  uint32_t y[4] = {0, 0, 0, 0};
+  uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0), lane gl = 0
+  int64_t lastnz = -1;
+  const uint32_t k15 = rk[3] >> 24;
+  const uint32_t gl_addr = (gl << 8) | lb;  // T0 address of byte value gl
+  const CtrCache cc = ctr_cache_build(nraw, gl, rk, rkr, lb);
+  const int gsrc = lane & ~(G - 1);
+  CtrCache cur{};
+
+  int64_t s_last = -1;  // the lane's last GHASH slot (1..m)
+  if (gl == 0) { if (m >= (uint32_t)G) s_last = (int64_t)(m / G) * G; }
+  else if (gl <= m) s_last = (int64_t)gl + (int64_t)((m - gl) / G) * G;
+  const uint32_t e_comb = s_last >= 1 ? S - (uint32_t)s_last : 1u;  // 1..G
+  uint32_t hp[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e_comb - 1][w];
+
+  for (uint32_t t = 0; t < steps; t++) {
+    const uint32_t base = t * (uint32_t)G;
+    if ((base & 255u) == 0u) {  // a new ctr >> 8 (the same for every slot of the step): its cache words
+      const int sl = gsrc + (int)(base >> 8);
+      cur.u0r = (uint32_t)__shfl((int)cc.u0r, sl, 64);
+      cur.k0 = (uint32_t)__shfl((int)cc.k0, sl, 64);
+      cur.k1r = (uint32_t)__shfl((int)cc.k1r, sl, 64);
+      cur.k2r = (uint32_t)__shfl((int)cc.k2r, sl, 64);
+      cur.k3 = (uint32_t)__shfl((int)cc.k3, sl, 64);
+    }
+    const uint32_t s = base + gl;
+    const bool fast = base >= (uint32_t)G && base + G <= fast_end;
+    if (__builtin_amdgcn_ballot_w64(!fast) == 0) {  // every group: whole data blocks only
+      const uint32_t off = (s - 2u) * 16u;
+      const uint4 Pu = ld16(src + off);
+      uint32_t st[4];
+      aes_ctr_r12(st, gl_addr ^ (((base & 0xffu) ^ k15) << 8), cur, lb);  // ctr = s
+      aes_rounds_tt<NR, 3>(st, rk, rkr, lb);
+      const uint32_t C[4] = {Pu.x ^ st[0], Pu.y ^ st[1], Pu.z ^ st[2], Pu.w ^ st[3]};
+      st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
+      if (OPEN) {
+        const int j = last_nonzero(C, 16);
+        if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((C[j >> 2] >> (8 * (j & 3))) & 0xffu);
+      }
+      ghash_mul<ATLS_GHASH_W>(y, wb);
+      if (OPEN) { y[0] ^= Pu.x; y[1] ^= Pu.y; y[2] ^= Pu.z; y[3] ^= Pu.w; }
+      else { y[0] ^= C[0]; y[1] ^= C[1]; y[2] ^= C[2]; y[3] ^= C[3]; }
+      continue;
+    }
+    // general step: slot 0 = E_K(J0), slot 1 = AAD, slots 2..m-1 data, slot m = length block
+    const bool data = s >= 2u && s + 1u <= m;
+    uint32_t P[4] = {0, 0, 0, 0};
+    if (data) {
+      const uint32_t off = (s - 2u) * 16u;
+      if (off + 16u <= len && src_al) {
+        const uint4 v = *reinterpret_cast<const uint4*>(src + off);
+        P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
+      } else {
+        const uint32_t valid = min(16u, n_aead - off);
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          if ((uint32_t)q < valid) {
+            const uint32_t byte = (off + q < len) ? src[off + q] : (uint32_t)d.content_type;  // record.rs:173
+            P[q >> 2] |= byte << (8 * (q & 3));
+          }
+        }
+      }
+    }
+    const uint32_t ctr = s > 1u ? s : 1u;  // J0 + (s - 1) for data slots
+    uint32_t st[4];
+    aes_ctr_r12(st, perm((ctr & 0xffu) ^ k15, lb, 0x0c0c0400u), cur, lb);
+    aes_rounds_tt<NR, 3>(st, rk, rkr, lb);
+    if (s == 0) { e0 = st[0]; e1 = st[1]; e2 = st[2]; e3 = st[3]; }
+    uint32_t B[4] = {0, 0, 0, 0};
+    if (s == 1u) {
+      B[0] = hdr0; B[1] = hdr1;
+    } else if (data) {
+      const uint32_t off = (s - 2u) * 16u;
+      const uint32_t valid = min(16u, n_aead - off);
+      uint32_t C[4] = {P[0] ^ st[0], P[1] ^ st[1], P[2] ^ st[2], P[3] ^ st[3]};
+      if (valid < 16) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) {
+          const int lo = 4 * w;
+          if ((int)valid < lo + 4) C[w] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
+        }
+      }
+      if (valid == 16 && dst_al) {
+        *reinterpret_cast<uint4*>(dst + off) = make_uint4(C[0], C[1], C[2], C[3]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; q++)
+          if ((uint32_t)q < valid) dst[off + q] = (uint8_t)get_byte(C, q);
+      }
+      if (OPEN) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) B[w] = P[w];
+        const int j = last_nonzero(C, (int)valid);
+        if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((C[j >> 2] >> (8 * (j & 3))) & 0xffu);
+      } else {
+#pragma unroll
+        for (int w = 0; w < 4; w++) B[w] = C[w];
+      }
+    } else if (s == m) {  // [len(A)]_64 || [len(C)]_64 in bits (gcm.rs:121)
+      const uint64_t cbits = (uint64_t)n_aead * 8u;
+      B[0] = 0; B[1] = bswap32(40u);
+      B[2] = bswap32((uint32_t)(cbits >> 32)); B[3] = bswap32((uint32_t)cbits);
+    }
+    uint32_t yn[4] = {y[0], y[1], y[2], y[3]};
+    if (base) ghash_mul<ATLS_GHASH_W>(yn, wb);
+    if (s >= 1u && s <= m) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) y[w] = yn[w] ^ B[w];
+    }
+  }
+
+  uint32_t z[4] = {0, 0, 0, 0};
+  if (s_last >= 1) {
+    const uint32_t yb[4] = {bswap32(y[0]), bswap32(y[1]), bswap32(y[2]), bswap32(y[3])};
+    gf_mul_comb(yb, hp, z);
+  }
+#pragma unroll
+  for (int w = 0; w < 4; w++) z[w] = group_xor<G>(z[w]);
+  const uint32_t t0 = e0 ^ bswap32(z[0]), t1 = e1 ^ bswap32(z[1]), t2 = e2 ^ bswap32(z[2]), t3 = e3 ^ bswap32(z[3]);
+  if (!OPEN) {
+    if (gl == 0) {
+      if (A.tags_out) st16(A.tags_out + 16ull * rec_idx, make_uint4(t0, t1, t2, t3));
+      if (wire) {  // header || ciphertext || tag (record.rs:175-197)
+        uint8_t* h = dst - 5;
+        h[0] = (uint8_t)hdr0; h[1] = (uint8_t)(hdr0 >> 8); h[2] = (uint8_t)(hdr0 >> 16);
+        h[3] = (uint8_t)(hdr0 >> 24); h[4] = (uint8_t)hdr1;
+        st16(dst + n_aead, make_uint4(t0, t1, t2, t3));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int off = G / 2; off >= 1; off >>= 1) {  // content-type scan (record.rs:229-237), group max
+      const int64_t o = __shfl_xor(lastnz, off, 64);
+      lastnz = o > lastnz ? o : lastnz;
+    }
+    if (gl == 0) {
+      const uint4 tg = ld16(wire ? src + len : A.tags_in + 16ull * rec_idx);
+      const bool ok = (tg.x == t0) & (tg.y == t1) & (tg.z == t2) & (tg.w == t3);
+      write_open_result(A, rec_idx, true, len, ok, lastnz, hdr_ok);
+    }
+  }
+}
+
+// One record by the whole wave (gcm_record), after the direct-mode descriptor check.
+template <int NR, bool OPEN>
+__device__ __forceinline__ void gcm_one(const GcmArgs& A, uint32_t r, uint32_t lb, uint32_t wb, int lane) {
+  {
+    atls_rec d = A.recs[r];
+    d.key_slot = uni(d.key_slot);
+    d.len = uni(d.len);
+    d.mode = (uint8_t)uni(d.mode);
+    if (!A.idx) {  // direct mode: reject as the plan would
+      const uint32_t st = uni(direct_reject(d, A.ks, A.n_slots, OPEN));
+      if (st) {
+        if (lane == 0) {
+          atomicOr(A.err, 1u);
+          if (OPEN) {
+            atls_open_result rr = {0, (uint8_t)st, 0, {0, 0}};
+            A.res[r] = rr;
+          }
+        }
+        return;
+      }
+    }
+    gcm_record<NR, OPEN>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
+    wave_lds_sync();  // table reads of this record done before the next record rebuilds it
+  }
+}
+
 // WAVES waves per workgroup (one record per wave at a time), one workgroup per CU: the LDS
 // footprint (64 KiB tables + 8 KiB per wave) is what limits residency. One launch per AES round
 // count (a kernel holds only that count's round keys); the waves take the records of that round
@@ -515,29 +780,35 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   const uint32_t lb = 4u * (uint32_t)(lane & 31);
   const uint32_t wb = (uint32_t)kTabBytes + (ATLS_DBG_SHARED_GHASH ? 0u : (uint32_t)wave * kGhashBytes);
   const WorkList W{A.idx, A.plan, NR == 10 ? kListGcm10 : NR == 12 ? kListGcm12 : kListGcm14, A.n};
-  const uint32_t cnt = uni(W.size());
   const uint32_t stride = gridDim.x * kWaves;
-  for (uint32_t q = blockIdx.x * kWaves + wave; q < cnt; q += stride) {
-    const uint32_t r = uni(W.record(q));
-    atls_rec d = A.recs[r];
-    d.key_slot = uni(d.key_slot);
-    d.len = uni(d.len);
-    d.mode = (uint8_t)uni(d.mode);
-    if (!A.idx) {  // direct mode: reject as the plan would
-      const uint32_t st = uni(direct_reject(d, A.ks, A.n_slots, OPEN));
-      if (st) {
-        if (lane == 0) {
-          atomicOr(A.err, 1u);
-          if (OPEN) {
-            atls_open_result rr = {0, (uint8_t)st, 0, {0, 0}};
-            A.res[r] = rr;
-          }
-        }
+  // Work units, taken round-robin. Key-grouped direct batch (A.gidx): first the same number of
+  // aligned kGroupPad-position runs per wave (lane groups where group_ok holds, single records
+  // otherwise), then the remaining positions one by one, so no wave ends more than a few records
+  // after another. Otherwise one unit per position of the work list.
+  constexpr uint32_t NG = 64 / kGroupLanes;
+  const bool grouped = A.gidx != nullptr;
+  const uint32_t npos = grouped ? uni(cptr(A.gcount)[0]) : uni(W.size());
+  const uint32_t qfull = grouped ? (npos / kGroupPad) / stride * stride : 0u;
+  const uint32_t n_units = qfull + (npos - kGroupPad * qfull);
+  for (uint32_t u = blockIdx.x * kWaves + wave; u < n_units; u += stride) {
+    const bool grp = u < qfull;
+    const uint32_t p0 = grp ? kGroupPad * u : kGroupPad * qfull + (u - qfull);
+    const uint32_t span = grp ? kGroupPad : 1u, step = grp ? NG : 1u;
+#pragma unroll 1
+    for (uint32_t h = 0; h < span; h += step) {
+      uint32_t key = 0;
+      if (grp && group_ok<OPEN, kGroupLanes>(A, A.gidx + p0 + h, NG, key)) {
+        const uint32_t mine = A.gidx[p0 + h + (uint32_t)lane / kGroupLanes];  // this lane group's record
+        gcm_group<NR, OPEN, kGroupLanes>(A, A.ks + key, mine, lb, wb, lane);
+        wave_lds_sync();
         continue;
       }
+#pragma unroll 1
+      for (uint32_t j = 0; j < step; j++) {
+        const uint32_t r = uni(grouped ? cptr(A.gidx)[p0 + h + j] : W.record(p0 + h + j));
+        if (r != kNoRecord) gcm_one<NR, OPEN>(A, r, lb, wb, lane);
+      }
     }
-    gcm_record<NR, OPEN>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
-    wave_lds_sync();  // table reads of this record done before the next record rebuilds it
   }
 }
 
@@ -545,14 +816,16 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
 
 // nr_mask: bit 0/1/2 = key slots with 10/12/14 rounds exist (one launch each). plan/idx: the
 // batch plan of atls_launch_plan, or idx = nullptr for a direct batch (one round count only; the
-// kernel validates and reports through err). grid: workgroups per launch (one per CU).
+// kernel validates and reports through err). gidx/gcount: a direct batch's key groups
+// (atls_launch_group) or nullptr. grid: workgroups per launch (one per CU).
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
-                               uint32_t* err, uint32_t n_slots, int nr_mask, int grid, hipStream_t s) {
+                               uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
+                               const uint32_t* gcount, int grid, hipStream_t s) {
   if (n == 0) return 0;
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, idx,
-                  (atls::PlanHdr*)plan, err, n_slots};
+                  (atls::PlanHdr*)plan, err, n_slots, idx ? nullptr : gidx, gcount};
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;

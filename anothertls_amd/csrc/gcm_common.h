@@ -206,6 +206,8 @@ struct GcmArgs {
   PlanHdr* plan;
   uint32_t* err;           // direct mode: sticky error word
   uint32_t n_slots;        // direct mode: key-table size
+  const uint32_t* gidx;    // direct mode: key groups (plan.hip atls_launch_group), or nullptr
+  const uint32_t* gcount;  // device word: positions in gidx
 };
 
 // Open result for one record (record.rs:203-240 decrypt + padding scan). lastnz = (position <<

@@ -34,6 +34,13 @@ struct WorkList {
   __device__ __forceinline__ uint32_t record(uint32_t pos) const { return idx ? idx[P->off[list] + pos] : pos; }
 };
 
+// Key groups of a direct AES-GCM batch (group_* kernels, plan.hip): record indices sorted by key
+// slot, each slot's run padded with kNoRecord to a multiple of kGroupPad positions, so an aligned
+// run of kGroupPad positions never holds two keys. gcm_kernel seals such runs in lane groups.
+constexpr uint32_t kNoRecord = 0xffffffffu;
+constexpr uint32_t kGroupPad = 4;
+constexpr uint32_t kGroupMaxSlots = 65536;  // larger key tables are not grouped (one-workgroup scan)
+
 // ChaCha20::encrypt counts its 64-byte blocks as (len as f32 / 64.0).ceil() (chacha20/cipher.rs:94),
 // exact only while the AEAD input is below 2^24 bytes. Longer ChaCha20-Poly1305 records are
 // refused (ILLEGAL_PARAMETER) instead of being sealed differently from the reference.

@@ -131,7 +131,68 @@ __global__ __launch_bounds__(256) void plan_scatter(uint32_t n, const uint8_t* k
   }
 }
 
+// ---- key groups (direct AES-GCM batches) ----------------------------------------------------
+// group_count -> group_scan -> group_scatter: a counting sort of the records by key slot (bucket
+// n_slots collects refused slots). cnt is all zero between batches: group_scan clears it.
+__global__ __launch_bounds__(256) void group_count(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t k = recs[i].key_slot;
+    atomicAdd(&cnt[k < n_slots ? k : n_slots], 1u);
+  }
+}
+
+__device__ __forceinline__ uint32_t pad_group(uint32_t c) { return (c + kGroupPad - 1u) / kGroupPad * kGroupPad; }
+
+// One workgroup: exclusive prefix of the padded bucket sizes -> cursors; the padding positions
+// get kNoRecord; *total = padded length of the list.
+__global__ __launch_bounds__(1024) void group_scan(uint32_t* cnt, uint32_t nb, uint32_t* cur, uint32_t* gidx,
+                                                   uint32_t* total) {
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (nb + blockDim.x - 1u) / blockDim.x, lo = min(nb, t * per), hi = min(nb, lo + per);
+  uint32_t sum = 0;
+  for (uint32_t b = lo; b < hi; b++) sum += pad_group(cnt[b]);
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < blockDim.x; d <<= 1) {
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+  for (uint32_t b = lo; b < hi; b++) {
+    const uint32_t c = cnt[b], pc = pad_group(c);
+    cur[b] = run;
+    for (uint32_t j = c; j < pc; j++) gidx[run + j] = kNoRecord;
+    cnt[b] = 0u;
+    run += pc;
+  }
+  if (t == blockDim.x - 1u) *total = part[t];
+}
+
+__global__ __launch_bounds__(256) void group_scatter(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cur,
+                                                     uint32_t* gidx) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t k = recs[i].key_slot;
+    gidx[atomicAdd(&cur[k < n_slots ? k : n_slots], 1u)] = i;
+  }
+}
+
 }  // namespace atls
+
+// Key groups of a direct batch: cnt / cur hold n_slots + 1 words (cnt zero on entry and on
+// return), gidx n + (kGroupPad - 1) * (n_slots + 1) words, total one word.
+extern "C" int atls_launch_group(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt, uint32_t* cur,
+                                 uint32_t* gidx, uint32_t* total, int cus, hipStream_t s) {
+  if (n_slots > atls::kGroupMaxSlots) return ATLS_INTERNAL_ERROR;
+  const uint32_t want = (n + 255u) / 256u, cap = (uint32_t)(cus > 0 ? 2 * cus : 512);
+  const uint32_t G = want ? (want < cap ? want : cap) : 1u;
+  hipLaunchKernelGGL(atls::group_count, dim3(G), dim3(256), 0, s, recs, n, n_slots, cnt);
+  hipLaunchKernelGGL(atls::group_scan, dim3(1), dim3(1024), 0, s, cnt, n_slots + 1u, cur, gidx, total);
+  hipLaunchKernelGGL(atls::group_scatter, dim3(G), dim3(256), 0, s, recs, n, n_slots, cur, gidx);
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}
 
 // P (device, PlanHdr), keys (n bytes), idx (n words) and wg (2 x 64 x kPlanMaxWG words) are
 // engine scratch.
