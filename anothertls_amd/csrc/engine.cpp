@@ -327,7 +327,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     if (!planned && e->group_min && n >= e->group_min && e->n_slots <= atls::kGroupMaxSlots) {
       const size_t nb = (size_t)e->n_slots + 1;
       const size_t cnt_cap = e->grp_cnt.cap;
-      if (!e->grp_cnt.reserve(4 * nb) || !e->grp_cur.reserve(4 * nb + 4) ||
+      if (!e->grp_cnt.reserve(4 * nb) || !e->grp_cur.reserve(4 * nb + 8) ||
           !e->grp_idx.reserve(4 * ((size_t)n + (atls::kGroupPad - 1) * nb)))
         return ATLS_INTERNAL_ERROR;
       // the counters are zero between batches (group_scan clears them): zero a new buffer once

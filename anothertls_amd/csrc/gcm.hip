@@ -510,6 +510,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 #define ATLS_GCM_GROUP_LANES 16
 #endif
 constexpr int kGroupLanes = ATLS_GCM_GROUP_LANES;
+#ifndef ATLS_GCM_GROUP_TAIL
+#define ATLS_GCM_GROUP_TAIL 2  // 2: units from a work counter, the last ~stride records as single records;
+                               // 1: round-robin, runs past the last whole round as single records; 0: all runs
+#endif
 static_assert(kGroupLanes == 16 || kGroupLanes == 32, "lane groups of 16 or 32");
 
 // XOR of x over the lane's G-lane group: DPP within 16-lane rows, then rows by readlane.
@@ -788,9 +792,19 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   constexpr uint32_t NG = 64 / kGroupLanes;
   const bool grouped = A.gidx != nullptr;
   const uint32_t npos = grouped ? uni(cptr(A.gcount)[0]) : uni(W.size());
-  const uint32_t qfull = grouped ? (npos / kGroupPad) / stride * stride : 0u;
+  const uint32_t nq = npos / kGroupPad;
+  const bool dyn = grouped && ATLS_GCM_GROUP_TAIL == 2;
+  const uint32_t tail_q = stride / kGroupPad;  // dynamic: about one single record per wave at the end
+  const uint32_t qfull = !grouped ? 0u
+                         : dyn ? (nq > tail_q ? nq - tail_q : 0u)
+                         : (ATLS_GCM_GROUP_TAIL ? nq / stride * stride : nq);
   const uint32_t n_units = qfull + (npos - kGroupPad * qfull);
-  for (uint32_t u = blockIdx.x * kWaves + wave; u < n_units; u += stride) {
+  auto next_unit = [&]() -> uint32_t {  // dynamic: the batch's work counter (cleared by group_scan)
+    uint32_t v = 0;
+    if (lane == 0) v = atomicAdd(A.gwork, 1u);
+    return uni(v);
+  };
+  for (uint32_t u = dyn ? next_unit() : blockIdx.x * kWaves + wave; u < n_units; u = dyn ? next_unit() : u + stride) {
     const bool grp = u < qfull;
     const uint32_t p0 = grp ? kGroupPad * u : kGroupPad * qfull + (u - qfull);
     const uint32_t span = grp ? kGroupPad : 1u, step = grp ? NG : 1u;
@@ -825,7 +839,8 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                const uint32_t* gcount, int grid, hipStream_t s) {
   if (n == 0) return 0;
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, idx,
-                  (atls::PlanHdr*)plan, err, n_slots, idx ? nullptr : gidx, gcount};
+                  (atls::PlanHdr*)plan, err, n_slots, idx ? nullptr : gidx, gcount,
+                  gcount ? const_cast<uint32_t*>(gcount) + 1 : nullptr};
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;

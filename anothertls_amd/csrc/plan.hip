@@ -144,7 +144,8 @@ __global__ __launch_bounds__(256) void group_count(const atls_rec* recs, uint32_
 __device__ __forceinline__ uint32_t pad_group(uint32_t c) { return (c + kGroupPad - 1u) / kGroupPad * kGroupPad; }
 
 // One workgroup: exclusive prefix of the padded bucket sizes -> cursors; the padding positions
-// get kNoRecord; *total = padded length of the list.
+// get kNoRecord; total[0] = padded length of the list, total[1] = 0 (the record kernel's work
+// counter).
 __global__ __launch_bounds__(1024) void group_scan(uint32_t* cnt, uint32_t nb, uint32_t* cur, uint32_t* gidx,
                                                    uint32_t* total) {
   __shared__ uint32_t part[1024];
@@ -168,7 +169,10 @@ __global__ __launch_bounds__(1024) void group_scan(uint32_t* cnt, uint32_t nb, u
     cnt[b] = 0u;
     run += pc;
   }
-  if (t == blockDim.x - 1u) *total = part[t];
+  if (t == blockDim.x - 1u) {
+    total[0] = part[t];
+    total[1] = 0u;
+  }
 }
 
 __global__ __launch_bounds__(256) void group_scatter(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cur,
@@ -182,7 +186,7 @@ __global__ __launch_bounds__(256) void group_scatter(const atls_rec* recs, uint3
 }  // namespace atls
 
 // Key groups of a direct batch: cnt / cur hold n_slots + 1 words (cnt zero on entry and on
-// return), gidx n + (kGroupPad - 1) * (n_slots + 1) words, total one word.
+// return), gidx n + (kGroupPad - 1) * (n_slots + 1) words, total two words.
 extern "C" int atls_launch_group(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt, uint32_t* cur,
                                  uint32_t* gidx, uint32_t* total, int cus, hipStream_t s) {
   if (n_slots > atls::kGroupMaxSlots) return ATLS_INTERNAL_ERROR;
