@@ -16,7 +16,7 @@
 
 namespace atls {
 
-// Per key slot device state, built by the key-setup kernel (keysetup.hip). 3136 B, 16-B aligned.
+// Per key slot device state, built by the key-setup kernel (keysetup.hip). 3648 B, 16-B aligned.
 struct alignas(16) KeySched {
   uint32_t suite, nr, key_len, valid;  // nr = AES rounds (10/12/14), 0 for ChaCha
   uint32_t rk[60];                     // AES round keys as raw words (cipher.rs:216-249 expanded_key)
@@ -27,9 +27,9 @@ struct alignas(16) KeySched {
   uint32_t p4_be[32][4];               // x^(4p) * H^64, p = 0..31: seeds of the 4-bit GHASH tables
   uint32_t rkr[60];                    // rotl16(rk[i]): the T-table rounds' key words (gcm.hip)
   uint32_t pad[4];
-  uint32_t p4g_be[2][32][4];           // x^(4p) * H^16 and x^(4p) * H^32: table seeds of grouped records
+  uint32_t p4g_be[3][32][4];           // x^(4p) * H^(8 << t): table seeds of records in lane groups
 };
-static_assert(sizeof(KeySched) == 3136, "KeySched must be 3136 B");
+static_assert(sizeof(KeySched) == 3648, "KeySched must be 3648 B");
 
 constexpr int kSuiteAes128 = 0x1301, kSuiteAes256 = 0x1302, kSuiteChacha = 0x1303;
 

@@ -506,23 +506,25 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 // multiplier is H^G (table from the key schedule's p4g seeds) and one lane combine, one table
 // build and one counter-cache build serve 64/G records. A 16 KiB record's 1,028 slots fill
 // 64.25 sixteen-lane steps instead of 16.06 wave steps plus a per-record tail, combine and table.
-#ifndef ATLS_GCM_GROUP_LANES
-#define ATLS_GCM_GROUP_LANES 16
+#ifndef ATLS_GCM_GROUP_LANES_128
+#define ATLS_GCM_GROUP_LANES_128 8  // lanes per AES-128 record in a lane group (8, 16 or 32)
 #endif
-constexpr int kGroupLanes = ATLS_GCM_GROUP_LANES;
-#ifndef ATLS_GCM_GROUP_TAIL
-#define ATLS_GCM_GROUP_TAIL 2  // 2: units from a work counter, the last ~stride records as single records;
-                               // 1: round-robin, runs past the last whole round as single records; 0: all runs
+#ifndef ATLS_GCM_GROUP_LANES_256
+#define ATLS_GCM_GROUP_LANES_256 16  // AES-192 / AES-256 records
 #endif
-static_assert(kGroupLanes == 16 || kGroupLanes == 32, "lane groups of 16 or 32");
+// 8 lanes measured faster for AES-128 (C2 854 -> 873 GiB/s) and slower for AES-256 (C4 790 ->
+// 745), same-box A/B (profiles/r02/ab_gcm_group_variants.log)
+template <int NR>
+constexpr int group_lanes() { return NR == 10 ? ATLS_GCM_GROUP_LANES_128 : ATLS_GCM_GROUP_LANES_256; }
 
-// XOR of x over the lane's G-lane group: DPP within 16-lane rows, then rows by readlane.
+
+// XOR of x over the lane's G-lane group: DPP within 8- / 16-lane rows, then rows by readlane.
 template <int G>
 __device__ __forceinline__ uint32_t group_xor(uint32_t x) {
   x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
   x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
   x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);
-  x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);
+  if (G >= 16) x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);
   if (G == 32) {
     const uint32_t a = (uint32_t)(__builtin_amdgcn_readlane((int)x, 0) ^ __builtin_amdgcn_readlane((int)x, 16));
     const uint32_t b = (uint32_t)(__builtin_amdgcn_readlane((int)x, 32) ^ __builtin_amdgcn_readlane((int)x, 48));
@@ -593,7 +595,7 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
   if (steps > 1u) {
     uint32_t seed[4];
 #pragma unroll
-    for (int w = 0; w < 4; w++) seed[w] = k->p4g_be[G == 16 ? 0 : 1][lane >> 1][w];
+    for (int w = 0; w < 4; w++) seed[w] = k->p4g_be[G == 8 ? 0 : G == 16 ? 1 : 2][lane >> 1][w];
     ghash_table_entries<8>(wb, seed, lane >> 1, (lane & 1) * 8);
     wave_lds_sync();
   }
@@ -771,7 +773,8 @@ __device__ __forceinline__ void gcm_one(const GcmArgs& A, uint32_t r, uint32_t l
 // WAVES waves per workgroup (one record per wave at a time), one workgroup per CU: the LDS
 // footprint (64 KiB tables + 8 KiB per wave) is what limits residency. One launch per AES round
 // count (a kernel holds only that count's round keys); the waves take the records of that round
-// count's work list (plan.hip, longest first) round-robin.
+// count's work list (plan.hip, longest first) round-robin, or a key-grouped direct batch's lane
+// groups from a work counter.
 template <bool OPEN, int kWaves, int NR>
 __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -785,43 +788,41 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   const uint32_t wb = (uint32_t)kTabBytes + (ATLS_DBG_SHARED_GHASH ? 0u : (uint32_t)wave * kGhashBytes);
   const WorkList W{A.idx, A.plan, NR == 10 ? kListGcm10 : NR == 12 ? kListGcm12 : kListGcm14, A.n};
   const uint32_t stride = gridDim.x * kWaves;
-  // Work units, taken round-robin. Key-grouped direct batch (A.gidx): first the same number of
-  // aligned kGroupPad-position runs per wave (lane groups where group_ok holds, single records
-  // otherwise), then the remaining positions one by one, so no wave ends more than a few records
-  // after another. Otherwise one unit per position of the work list.
+  if (!A.gidx) {  // one record per wave, positions of the work list round-robin
+    const uint32_t cnt = uni(W.size());
+    for (uint32_t q = blockIdx.x * kWaves + wave; q < cnt; q += stride) gcm_one<NR, OPEN>(A, uni(W.record(q)), lb, wb, lane);
+    return;
+  }
+  // Key-grouped direct batch: units from the batch's work counter (cleared by group_scan). Unit u
+  // < nrun is the lane-group run at positions NG*u .. NG*u+NG-1 (aligned: the plan pads each key's
+  // records to kGroupPad), sealed as one lane group when group_ok holds, record by record
+  // otherwise; the last ~stride positions go one per unit, so the waves finish within about one
+  // record of each other. (Round-robin units instead: C4 688 vs 782 GiB/s, same-box A/B.)
+  constexpr int kGroupLanes = group_lanes<NR>();
+  static_assert(kGroupLanes == 8 || kGroupLanes == 16 || kGroupLanes == 32, "lane groups of 8, 16 or 32");
+  static_assert(kGroupPad % (64 / kGroupLanes) == 0, "the plan's runs hold whole lane groups");
   constexpr uint32_t NG = 64 / kGroupLanes;
-  const bool grouped = A.gidx != nullptr;
-  const uint32_t npos = grouped ? uni(cptr(A.gcount)[0]) : uni(W.size());
-  const uint32_t nq = npos / kGroupPad;
-  const bool dyn = grouped && ATLS_GCM_GROUP_TAIL == 2;
-  const uint32_t tail_q = stride / kGroupPad;  // dynamic: about one single record per wave at the end
-  const uint32_t qfull = !grouped ? 0u
-                         : dyn ? (nq > tail_q ? nq - tail_q : 0u)
-                         : (ATLS_GCM_GROUP_TAIL ? nq / stride * stride : nq);
-  const uint32_t n_units = qfull + (npos - kGroupPad * qfull);
-  auto next_unit = [&]() -> uint32_t {  // dynamic: the batch's work counter (cleared by group_scan)
+  const uint32_t npos = uni(cptr(A.gcount)[0]);
+  const uint32_t nq = npos / NG, tail_q = stride / NG;
+  const uint32_t nrun = nq > tail_q ? nq - tail_q : 0u;
+  const uint32_t n_units = nrun + (npos - NG * nrun);
+  for (;;) {
     uint32_t v = 0;
     if (lane == 0) v = atomicAdd(A.gwork, 1u);
-    return uni(v);
-  };
-  for (uint32_t u = dyn ? next_unit() : blockIdx.x * kWaves + wave; u < n_units; u = dyn ? next_unit() : u + stride) {
-    const bool grp = u < qfull;
-    const uint32_t p0 = grp ? kGroupPad * u : kGroupPad * qfull + (u - qfull);
-    const uint32_t span = grp ? kGroupPad : 1u, step = grp ? NG : 1u;
+    const uint32_t u = uni(v);
+    if (u >= n_units) break;
+    uint32_t key = 0;
+    if (u < nrun && group_ok<OPEN, kGroupLanes>(A, A.gidx + NG * u, NG, key)) {
+      const uint32_t mine = A.gidx[NG * u + (uint32_t)lane / kGroupLanes];  // this lane group's record
+      gcm_group<NR, OPEN, kGroupLanes>(A, A.ks + key, mine, lb, wb, lane);
+      wave_lds_sync();
+      continue;
+    }
+    const uint32_t p0 = u < nrun ? NG * u : NG * nrun + (u - nrun), cnt = u < nrun ? NG : 1u;
 #pragma unroll 1
-    for (uint32_t h = 0; h < span; h += step) {
-      uint32_t key = 0;
-      if (grp && group_ok<OPEN, kGroupLanes>(A, A.gidx + p0 + h, NG, key)) {
-        const uint32_t mine = A.gidx[p0 + h + (uint32_t)lane / kGroupLanes];  // this lane group's record
-        gcm_group<NR, OPEN, kGroupLanes>(A, A.ks + key, mine, lb, wb, lane);
-        wave_lds_sync();
-        continue;
-      }
-#pragma unroll 1
-      for (uint32_t j = 0; j < step; j++) {
-        const uint32_t r = uni(grouped ? cptr(A.gidx)[p0 + h + j] : W.record(p0 + h + j));
-        if (r != kNoRecord) gcm_one<NR, OPEN>(A, r, lb, wb, lane);
-      }
+    for (uint32_t j = 0; j < cnt; j++) {
+      const uint32_t r = uni(cptr(A.gidx)[p0 + j]);
+      if (r != kNoRecord) gcm_one<NR, OPEN>(A, r, lb, wb, lane);
     }
   }
 }

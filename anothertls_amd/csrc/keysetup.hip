@@ -101,14 +101,14 @@ __global__ void key_setup_kernel(const atls_key* __restrict__ keys, uint32_t n, 
     gf_mul_be(p, h, q);
     for (int w = 0; w < 4; w++) p[w] = q[w];
   }
-  // p4[j] = x^(4j) * H^64; p4g[t][j] = x^(4j) * H^(16 << t) (records processed in lane groups)
+  // p4[j] = x^(4j) * H^64; p4g[t][j] = x^(4j) * H^(8 << t) (records processed in lane groups)
   uint32_t v[4] = {o->hpow_be[63][0], o->hpow_be[63][1], o->hpow_be[63][2], o->hpow_be[63][3]};
   for (int j = 0; j < 32; j++) {
     for (int w = 0; w < 4; w++) o->p4_be[j][w] = v[w];
     gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v);
   }
-  for (int t = 0; t < 2; t++) {
-    for (int w = 0; w < 4; w++) v[w] = o->hpow_be[(16 << t) - 1][w];
+  for (int t = 0; t < 3; t++) {
+    for (int w = 0; w < 4; w++) v[w] = o->hpow_be[(8 << t) - 1][w];
     for (int j = 0; j < 32; j++) {
       for (int w = 0; w < 4; w++) o->p4g_be[t][j][w] = v[w];
       gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v);

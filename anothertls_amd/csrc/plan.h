@@ -38,7 +38,7 @@ struct WorkList {
 // slot, each slot's run padded with kNoRecord to a multiple of kGroupPad positions, so an aligned
 // run of kGroupPad positions never holds two keys. gcm_kernel seals such runs in lane groups.
 constexpr uint32_t kNoRecord = 0xffffffffu;
-constexpr uint32_t kGroupPad = 4;
+constexpr uint32_t kGroupPad = 8;  // a run = the records of one wave at 8 lanes each
 constexpr uint32_t kGroupMaxSlots = 65536;  // larger key tables are not grouped (one-workgroup scan)
 
 // ChaCha20::encrypt counts its 64-byte blocks as (len as f32 / 64.0).ceil() (chacha20/cipher.rs:94),
