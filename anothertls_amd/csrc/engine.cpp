@@ -34,9 +34,10 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
-                               const uint32_t* gcount, int grid, hipStream_t s);
-extern "C" int atls_launch_group(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt, uint32_t* cur,
-                                 uint32_t* gidx, uint32_t* total, int cus, hipStream_t s);
+                               const uint32_t* ghdr, int grid, hipStream_t s);
+extern "C" size_t atls_group_hdr_offset(uint32_t n_slots);
+extern "C" int atls_launch_group(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt, void* aux,
+                                 uint32_t* gidx, int cus, hipStream_t s);
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
@@ -84,7 +85,7 @@ struct atls_engine {
   int aes_nr_mask = 0;                       // bit 0/1/2: AES slots with 10/12/14 rounds
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
   DevBuf plan, plan_keys, plan_idx, plan_wg; // batch plan (plan.hip)
-  DevBuf grp_cnt, grp_cur, grp_idx;          // key groups of direct AES-GCM batches (plan.hip)
+  DevBuf grp_cnt, grp_aux, grp_idx;          // key groups of direct AES-GCM batches (plan.hip)
   uint32_t group_min = 2048;                 // ATLS_GCM_GROUP_MIN: smallest batch to group (0: never)
   int chacha_wgs = 8;                        // ATLS_CHACHA_WGS: ChaCha20-Poly1305 workgroups per CU
   bool force_plan = false;                   // ATLS_FORCE_PLAN=1: plan every batch (tests)
@@ -323,26 +324,25 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     // A direct batch large enough: records of one key slot go through the kernel in lane groups
     // (gcm.hip gcm_group), after a counting sort by key slot (three small launches).
     const uint32_t* gidx = nullptr;
-    const uint32_t* gcount = nullptr;
+    const uint32_t* ghdr = nullptr;
     if (!planned && e->group_min && n >= e->group_min && e->n_slots <= atls::kGroupMaxSlots) {
-      const size_t nb = (size_t)e->n_slots + 1;
+      const size_t nb = (size_t)e->n_slots + 1, hdr_at = atls_group_hdr_offset(e->n_slots);
       const size_t cnt_cap = e->grp_cnt.cap;
-      if (!e->grp_cnt.reserve(4 * nb) || !e->grp_cur.reserve(4 * nb + 8) ||
-          !e->grp_idx.reserve(4 * ((size_t)n + (atls::kGroupPad - 1) * nb)))
+      if (!e->grp_cnt.reserve(8 * nb) || !e->grp_aux.reserve(hdr_at + sizeof(atls::GroupHdr) + 4 * (size_t)n) ||
+          !e->grp_idx.reserve(4 * (size_t)n))
         return ATLS_INTERNAL_ERROR;
-      // the counters are zero between batches (group_scan clears them): zero a new buffer once
+      // counts and cursors are zero between batches (group_place clears them): zero a new buffer once
       if (e->grp_cnt.cap != cnt_cap && hipMemsetAsync(e->grp_cnt.p, 0, e->grp_cnt.cap, s) != hipSuccess)
         return ATLS_INTERNAL_ERROR;
-      uint32_t* total = (uint32_t*)e->grp_cur.p + nb;
-      rc = atls_launch_group(d_recs, n, e->n_slots, (uint32_t*)e->grp_cnt.p, (uint32_t*)e->grp_cur.p,
-                             (uint32_t*)e->grp_idx.p, total, e->cus, s);
+      rc = atls_launch_group(d_recs, n, e->n_slots, (uint32_t*)e->grp_cnt.p, e->grp_aux.p, (uint32_t*)e->grp_idx.p,
+                             e->cus, s);
       if (rc) return rc;
       gidx = (const uint32_t*)e->grp_idx.p;
-      gcount = total;
+      ghdr = (const uint32_t*)((const uint8_t*)e->grp_aux.p + hdr_at);
     }
     rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, idx, e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask,
-                         gidx, gcount, e->cus, s);
+                         gidx, ghdr, e->cus, s);
   }
   if (rc) return rc;
   if (side && hipStreamWaitEvent(s, e->ev_side, 0) != hipSuccess) return ATLS_INTERNAL_ERROR;
@@ -644,7 +644,7 @@ void atls_engine_destroy(atls_engine* e) {
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   for (DevBuf* b : {&e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
                     &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx, &e->plan_wg,
-                    &e->grp_cnt, &e->grp_cur, &e->grp_idx})
+                    &e->grp_cnt, &e->grp_aux, &e->grp_idx})
     b->release();
   if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);
   if (e->ev_side) (void)hipEventDestroy(e->ev_side);

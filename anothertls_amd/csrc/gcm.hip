@@ -514,6 +514,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 #endif
 // 8 lanes measured faster for AES-128 (C2 854 -> 873 GiB/s) and slower for AES-256 (C4 790 ->
 // 745), same-box A/B (profiles/r02/ab_gcm_group_variants.log)
+#ifndef ATLS_GROUP_SHARES
+#define ATLS_GROUP_SHARES 1  // work counters of a grouped batch (1..8): shares of region A by blockIdx % shares
+                             // (8 measured no faster than 1: C2 850 vs 857 GiB/s, same-box A/B)
+#endif
 template <int NR>
 constexpr int group_lanes() { return NR == 10 ? ATLS_GCM_GROUP_LANES_128 : ATLS_GCM_GROUP_LANES_256; }
 
@@ -533,7 +537,7 @@ __device__ __forceinline__ uint32_t group_xor(uint32_t x) {
   return x;
 }
 
-// Whether the records r[0..NG) form a lane group: all present and accepted, one key slot, TLS or
+// Whether the records at pos[0..ng) form a lane group: all accepted, one key slot, TLS or
 // WIRE framing, the same number of G-slot steps, and few enough steps for the counter cache
 // (lane gl holds ctr >> 8 = gl). Wave-uniform.
 template <bool OPEN, int G>
@@ -541,7 +545,7 @@ __device__ __forceinline__ bool group_ok(const GcmArgs& A, const uint32_t* pos, 
   uint32_t steps0 = 0;
   for (uint32_t j = 0; j < ng; j++) {
     const uint32_t r = uni(cptr(pos)[j]);
-    if (r == kNoRecord) return false;
+    if (r >= A.n) return false;
     const atls_rec d = A.recs[r];
     if (direct_reject(d, A.ks, A.n_slots, OPEN) || d.mode == ATLS_MODE_RAW) return false;
     if (j == 0) key = d.key_slot;
@@ -793,36 +797,49 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
     for (uint32_t q = blockIdx.x * kWaves + wave; q < cnt; q += stride) gcm_one<NR, OPEN>(A, uni(W.record(q)), lb, wb, lane);
     return;
   }
-  // Key-grouped direct batch: units from the batch's work counter (cleared by group_scan). Unit u
-  // < nrun is the lane-group run at positions NG*u .. NG*u+NG-1 (aligned: the plan pads each key's
-  // records to kGroupPad), sealed as one lane group when group_ok holds, record by record
-  // otherwise; the last ~stride positions go one per unit, so the waves finish within about one
-  // record of each other. (Round-robin units instead: C4 688 vs 782 GiB/s, same-box A/B.)
+  // Key-grouped direct batch (plan.h): region B (records that form no lane group) round-robin
+  // first, then region A's lane-group runs from a work counter (ATLS_GROUP_SHARES counters over
+  // shares of the runs), the last ~stride records one per unit, so the waves finish within about
+  // one record of each other. (Round-robin runs instead: C4 688 vs 782 GiB/s, same-box A/B.)
   constexpr int kGroupLanes = group_lanes<NR>();
   static_assert(kGroupLanes == 8 || kGroupLanes == 16 || kGroupLanes == 32, "lane groups of 8, 16 or 32");
-  static_assert(kGroupPad % (64 / kGroupLanes) == 0, "the plan's runs hold whole lane groups");
+  static_assert(kGroupRun % (64 / kGroupLanes) == 0, "the plan's runs hold whole lane groups");
   constexpr uint32_t NG = 64 / kGroupLanes;
-  const uint32_t npos = uni(cptr(A.gcount)[0]);
-  const uint32_t nq = npos / NG, tail_q = stride / NG;
-  const uint32_t nrun = nq > tail_q ? nq - tail_q : 0u;
-  const uint32_t n_units = nrun + (npos - NG * nrun);
+  const uint32_t n_a = uni(cptr(&A.ghdr->n_a)[0]), n_b = uni(cptr(&A.ghdr->n_b)[0]);
+  {
+    uint32_t p = blockIdx.x * kWaves + wave;
+    uint32_t r = p < n_b ? uni(cptr(A.gidx)[n_a + p]) : 0u;
+    for (; p < n_b; p += stride) {
+      const uint32_t rn = p + stride < n_b ? uni(cptr(A.gidx)[n_a + p + stride]) : 0u;  // next index, early
+      if (r < A.n) gcm_one<NR, OPEN>(A, r, lb, wb, lane);  // (the plan writes indices < n only)
+      r = rn;
+    }
+  }
+  const uint32_t nx = gridDim.x < (uint32_t)ATLS_GROUP_SHARES ? gridDim.x : (uint32_t)ATLS_GROUP_SHARES;
+  const uint32_t x = blockIdx.x % nx;
+  const uint32_t nq = n_a / NG;  // runs (n_a is a multiple of kGroupRun)
+  const uint32_t q0 = (uint32_t)((uint64_t)nq * x / nx), sq = (uint32_t)((uint64_t)nq * (x + 1u) / nx) - q0;
+  const uint32_t tail_q = stride / nx / NG;
+  const uint32_t nrun = sq > tail_q ? sq - tail_q : 0u;
+  const uint32_t n_units = nrun + NG * (sq - nrun);
+  if (n_units == 0) return;
   for (;;) {
     uint32_t v = 0;
-    if (lane == 0) v = atomicAdd(A.gwork, 1u);
+    if (lane == 0) v = atomicAdd(&A.ghdr->work[x], 1u);
     const uint32_t u = uni(v);
     if (u >= n_units) break;
     uint32_t key = 0;
-    if (u < nrun && group_ok<OPEN, kGroupLanes>(A, A.gidx + NG * u, NG, key)) {
-      const uint32_t mine = A.gidx[NG * u + (uint32_t)lane / kGroupLanes];  // this lane group's record
+    if (u < nrun && group_ok<OPEN, kGroupLanes>(A, A.gidx + NG * (q0 + u), NG, key)) {
+      const uint32_t mine = A.gidx[NG * (q0 + u) + (uint32_t)lane / kGroupLanes];  // this lane group's record
       gcm_group<NR, OPEN, kGroupLanes>(A, A.ks + key, mine, lb, wb, lane);
       wave_lds_sync();
       continue;
     }
-    const uint32_t p0 = u < nrun ? NG * u : NG * nrun + (u - nrun), cnt = u < nrun ? NG : 1u;
+    const uint32_t p0 = u < nrun ? NG * (q0 + u) : NG * (q0 + nrun) + (u - nrun), cnt = u < nrun ? NG : 1u;
 #pragma unroll 1
     for (uint32_t j = 0; j < cnt; j++) {
       const uint32_t r = uni(cptr(A.gidx)[p0 + j]);
-      if (r != kNoRecord) gcm_one<NR, OPEN>(A, r, lb, wb, lane);
+      if (r < A.n) gcm_one<NR, OPEN>(A, r, lb, wb, lane);
     }
   }
 }
@@ -831,17 +848,17 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
 
 // nr_mask: bit 0/1/2 = key slots with 10/12/14 rounds exist (one launch each). plan/idx: the
 // batch plan of atls_launch_plan, or idx = nullptr for a direct batch (one round count only; the
-// kernel validates and reports through err). gidx/gcount: a direct batch's key groups
+// kernel validates and reports through err). gidx/ghdr: a direct batch's key groups
 // (atls_launch_group) or nullptr. grid: workgroups per launch (one per CU).
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
-                               const uint32_t* gcount, int grid, hipStream_t s) {
+                               const uint32_t* ghdr, int grid, hipStream_t s) {
   if (n == 0) return 0;
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, idx,
-                  (atls::PlanHdr*)plan, err, n_slots, idx ? nullptr : gidx, gcount,
-                  gcount ? const_cast<uint32_t*>(gcount) + 1 : nullptr};
+                  (atls::PlanHdr*)plan, err, n_slots, idx ? nullptr : gidx,
+                  (atls::GroupHdr*)const_cast<uint32_t*>(ghdr)};
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;

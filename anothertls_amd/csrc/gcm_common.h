@@ -207,8 +207,7 @@ struct GcmArgs {
   uint32_t* err;           // direct mode: sticky error word
   uint32_t n_slots;        // direct mode: key-table size
   const uint32_t* gidx;    // direct mode: key groups (plan.hip atls_launch_group), or nullptr
-  const uint32_t* gcount;  // device word: positions in gidx
-  uint32_t* gwork;         // device word after gcount: the grouped batch's work counter
+  GroupHdr* ghdr;          // their region sizes and work counters
 };
 
 // Open result for one record (record.rs:203-240 decrypt + padding scan). lastnz = (position <<

@@ -34,12 +34,18 @@ struct WorkList {
   __device__ __forceinline__ uint32_t record(uint32_t pos) const { return idx ? idx[P->off[list] + pos] : pos; }
 };
 
-// Key groups of a direct AES-GCM batch (group_* kernels, plan.hip): record indices sorted by key
-// slot, each slot's run padded with kNoRecord to a multiple of kGroupPad positions, so an aligned
-// run of kGroupPad positions never holds two keys. gcm_kernel seals such runs in lane groups.
-constexpr uint32_t kNoRecord = 0xffffffffu;
-constexpr uint32_t kGroupPad = 8;  // a run = the records of one wave at 8 lanes each
-constexpr uint32_t kGroupMaxSlots = 65536;  // larger key tables are not grouped (one-workgroup scan)
+// Key groups of a direct AES-GCM batch (group_* kernels, plan.hip): the record indices in two
+// regions. Region A: for every key slot, floor(count / kGroupRun) * kGroupRun of its records, so
+// every aligned run of kGroupRun positions holds one key (a lane group for gcm.hip gcm_group).
+// Region B: the rest (a slot's remainder, refused slots), compact. Nothing is padded.
+constexpr uint32_t kGroupRun = 8;  // the records of one wave at 8 lanes each
+constexpr uint32_t kGroupMaxSlots = 1u << 24;  // larger key tables are not grouped (per-slot scratch)
+// Group plan header after the per-slot arrays (atls_launch_group).
+struct GroupHdr {
+  uint32_t n_a, n_b;  // region sizes
+  uint32_t work[8];   // work counters of the record kernel, one per XCD share of region A
+  uint32_t pad[2];
+};
 
 // ChaCha20::encrypt counts its 64-byte blocks as (len as f32 / 64.0).ceil() (chacha20/cipher.rs:94),
 // exact only while the AEAD input is below 2^24 bytes. Longer ChaCha20-Poly1305 records are

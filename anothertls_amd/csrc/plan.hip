@@ -132,69 +132,106 @@ __global__ __launch_bounds__(256) void plan_scatter(uint32_t n, const uint8_t* k
 }
 
 // ---- key groups (direct AES-GCM batches) ----------------------------------------------------
-// group_count -> group_scan -> group_scatter: a counting sort of the records by key slot (bucket
-// n_slots collects refused slots). cnt is all zero between batches: group_scan clears it.
-__global__ __launch_bounds__(256) void group_count(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt) {
+// group_count -> group_alloc -> group_place: a counting sort of the records by key slot (bucket
+// n_slots collects refused slots) into the two regions of plan.h, without a pass over the key
+// table: the first record of each slot (its rank 0) reserves the slot's ranges in both regions,
+// one atomic per workgroup on the region sizes. cnt / cur are all zero between batches
+// (group_place clears them).
+struct GroupSlots {  // per-slot scratch, nb = n_slots + 1 entries each
+  uint32_t *cnt, *cur, *base_a, *base_b, *full;
+};
+
+__global__ __launch_bounds__(256) void group_count(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt,
+                                                   GroupHdr* hdr) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    hdr->n_a = hdr->n_b = 0u;
+    for (int x = 0; x < 8; x++) hdr->work[x] = 0u;
+  }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t k = recs[i].key_slot;
     atomicAdd(&cnt[k < n_slots ? k : n_slots], 1u);
   }
 }
 
-__device__ __forceinline__ uint32_t pad_group(uint32_t c) { return (c + kGroupPad - 1u) / kGroupPad * kGroupPad; }
-
-// One workgroup: exclusive prefix of the padded bucket sizes -> cursors; the padding positions
-// get kNoRecord; total[0] = padded length of the list, total[1] = 0 (the record kernel's work
-// counter).
-__global__ __launch_bounds__(1024) void group_scan(uint32_t* cnt, uint32_t nb, uint32_t* cur, uint32_t* gidx,
-                                                   uint32_t* total) {
-  __shared__ uint32_t part[1024];
+// rank[i] = record i's rank among its slot's records; rank 0 reserves the slot's ranges.
+__global__ __launch_bounds__(256) void group_alloc(const atls_rec* recs, uint32_t n, uint32_t n_slots, GroupSlots S,
+                                                   GroupHdr* hdr, uint32_t* rank) {
+  __shared__ uint32_t sa[256], sb[256], base[2];
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (nb + blockDim.x - 1u) / blockDim.x, lo = min(nb, t * per), hi = min(nb, lo + per);
-  uint32_t sum = 0;
-  for (uint32_t b = lo; b < hi; b++) sum += pad_group(cnt[b]);
-  part[t] = sum;
-  __syncthreads();
-  for (uint32_t d = 1; d < blockDim.x; d <<= 1) {
-    const uint32_t v = t >= d ? part[t - d] : 0u;
+  for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gridDim.x * blockDim.x) {  // block-uniform trip count
+    const uint32_t i = i0 + t;
+    uint32_t b = 0, j = 1, fa = 0, fb = 0;
+    if (i < n) {
+      const uint32_t k = recs[i].key_slot;
+      b = k < n_slots ? k : n_slots;
+      j = atomicAdd(&S.cur[b], 1u);
+      rank[i] = j;
+      if (j == 0) {
+        const uint32_t c = S.cnt[b];
+        fa = b < n_slots ? c / kGroupRun * kGroupRun : 0u;  // refused slots: all to region B
+        fb = c - fa;
+      }
+    }
+    sa[t] = fa;
+    sb[t] = fb;
     __syncthreads();
-    part[t] += v;
+    for (uint32_t d = 1; d < blockDim.x; d <<= 1) {  // inclusive scan of the reservations
+      const uint32_t va = t >= d ? sa[t - d] : 0u, vb = t >= d ? sb[t - d] : 0u;
+      __syncthreads();
+      sa[t] += va;
+      sb[t] += vb;
+      __syncthreads();
+    }
+    if (t == blockDim.x - 1u) {
+      base[0] = sa[t] ? atomicAdd(&hdr->n_a, sa[t]) : 0u;
+      base[1] = sb[t] ? atomicAdd(&hdr->n_b, sb[t]) : 0u;
+    }
     __syncthreads();
-  }
-  uint32_t run = part[t] - sum;
-  for (uint32_t b = lo; b < hi; b++) {
-    const uint32_t c = cnt[b], pc = pad_group(c);
-    cur[b] = run;
-    for (uint32_t j = c; j < pc; j++) gidx[run + j] = kNoRecord;
-    cnt[b] = 0u;
-    run += pc;
-  }
-  if (t == blockDim.x - 1u) {
-    total[0] = part[t];
-    total[1] = 0u;
+    if (j == 0) {
+      S.base_a[b] = base[0] + sa[t] - fa;
+      S.base_b[b] = base[1] + sb[t] - fb;
+      S.full[b] = fa;
+    }
+    __syncthreads();  // sa / sb / base reused
   }
 }
 
-__global__ __launch_bounds__(256) void group_scatter(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cur,
-                                                     uint32_t* gidx) {
+__global__ __launch_bounds__(256) void group_place(const atls_rec* recs, uint32_t n, uint32_t n_slots, GroupSlots S,
+                                                   const GroupHdr* hdr, const uint32_t* rank, uint32_t* gidx) {
+  const uint32_t n_a = hdr->n_a;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t k = recs[i].key_slot;
-    gidx[atomicAdd(&cur[k < n_slots ? k : n_slots], 1u)] = i;
+    const uint32_t k = recs[i].key_slot, b = k < n_slots ? k : n_slots;
+    const uint32_t j = rank[i], f = S.full[b];
+    const uint32_t pos = j < f ? S.base_a[b] + j : n_a + S.base_b[b] + (j - f);
+    if (pos < n) gidx[pos] = i;  // always true while cnt / cur start the batch at zero
+    S.cnt[b] = 0u;  // every record of the slot writes the same zeros; nothing here reads them
+    S.cur[b] = 0u;
   }
 }
 
 }  // namespace atls
 
-// Key groups of a direct batch: cnt / cur hold n_slots + 1 words (cnt zero on entry and on
-// return), gidx n + (kGroupPad - 1) * (n_slots + 1) words, total two words.
-extern "C" int atls_launch_group(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt, uint32_t* cur,
-                                 uint32_t* gidx, uint32_t* total, int cus, hipStream_t s) {
+// Key groups of a direct batch. cnt: 2 * (n_slots + 1) words (counts, cursors), zero on entry and
+// on return. aux: 3 arrays of n_slots + 1 words followed by the GroupHdr (atls_group_hdr_offset
+// bytes in), then n words of record ranks. gidx: n words.
+extern "C" size_t atls_group_hdr_offset(uint32_t n_slots) {
+  return (3u * ((size_t)n_slots + 1u) * 4u + 15u) / 16u * 16u;
+}
+
+extern "C" int atls_launch_group(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt, void* aux,
+                                 uint32_t* gidx, int cus, hipStream_t s) {
   if (n_slots > atls::kGroupMaxSlots) return ATLS_INTERNAL_ERROR;
+  const uint32_t nb = n_slots + 1u;
+  uint32_t* w = (uint32_t*)aux;
+  atls::GroupSlots S{cnt, cnt + nb, w, w + nb, w + 2 * nb};
+  auto* hdr = (atls::GroupHdr*)((uint8_t*)aux + atls_group_hdr_offset(n_slots));
+  uint32_t* rank = (uint32_t*)(hdr + 1);
   const uint32_t want = (n + 255u) / 256u, cap = (uint32_t)(cus > 0 ? 2 * cus : 512);
   const uint32_t G = want ? (want < cap ? want : cap) : 1u;
-  hipLaunchKernelGGL(atls::group_count, dim3(G), dim3(256), 0, s, recs, n, n_slots, cnt);
-  hipLaunchKernelGGL(atls::group_scan, dim3(1), dim3(1024), 0, s, cnt, n_slots + 1u, cur, gidx, total);
-  hipLaunchKernelGGL(atls::group_scatter, dim3(G), dim3(256), 0, s, recs, n, n_slots, cur, gidx);
+  hipLaunchKernelGGL(atls::group_count, dim3(G), dim3(256), 0, s, recs, n, n_slots, cnt, hdr);
+  hipLaunchKernelGGL(atls::group_alloc, dim3(G), dim3(256), 0, s, recs, n, n_slots, S, hdr, rank);
+  hipLaunchKernelGGL(atls::group_place, dim3(G), dim3(256), 0, s, recs, n, n_slots, S, (const atls::GroupHdr*)hdr,
+                     (const uint32_t*)rank, gidx);
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
 

@@ -1,8 +1,8 @@
 """GPU: key-grouped direct AES-GCM batches. A direct batch's records are counting-sorted by key
-slot (plan.hip atls_launch_group) and aligned runs of records that share a key and a step count
-are sealed / opened by one wavefront in lane groups (gcm.hip gcm_group); everything else (odd
-multiplicities, unequal lengths, RAW records, refused descriptors, records past the counter cache)
-takes the one-record-per-wave path. The results must not depend on the grouping: every case is
+slot (plan.hip atls_launch_group): whole runs of 8 records of one key first, the rest after. Runs
+whose records share a step count are sealed / opened by one wavefront in lane groups (gcm.hip
+gcm_group); everything else (a key's remainder, unequal lengths, RAW records, refused
+descriptors, records past the counter cache) takes the one-record-per-wave path. The results must not depend on the grouping: every case is
 compared byte for byte with the same batch run ungrouped (ATLS_GCM_GROUP_MIN=0) and with the
 oracle. Reference: crypto/aes/gcm.rs:42-128, net/record.rs:162-240."""
 import os
@@ -190,3 +190,25 @@ def test_c2_layout_grouped_equals_ungrouped():
     out_g, tags_g, _ = _seal(True, b["keys"], b["recs"], inbuf, b["out_bytes"])
     out_u, tags_u, _ = _seal(False, b["keys"], b["recs"], inbuf, b["out_bytes"])
     assert np.array_equal(tags_g, tags_u) and np.array_equal(out_g, out_u)
+
+
+def test_many_key_slots_both_regions():
+    """30,000 key slots (several scan tiles in group_scan), slot k holding k % 11 records of a
+    length set per slot: runs of 8 and remainders in both regions; equal to the ungrouped run
+    and to the oracle on a sample."""
+    n_keys = 30000
+    per_key = np.arange(n_keys) % 11
+    slot = np.repeat(np.arange(n_keys, dtype=np.uint32), per_key)
+    rng = np.random.default_rng(8)
+    slot = slot[rng.permutation(len(slot))]
+    n = len(slot)
+    lens = np.array([64, 100, 1000, 3000], np.uint64)[slot % 4]
+    b = workload.tls_batch(n, lens, 0x1301, n_keys=n_keys, shrink_keys=False)
+    b["recs"]["key_slot"] = slot
+    inbuf = rng.integers(0, 256, b["in_bytes"] + 64, dtype=np.uint8)
+    out_g, tags_g, _ = _seal(True, b["keys"], b["recs"], inbuf, b["out_bytes"])
+    out_u, tags_u, _ = _seal(False, b["keys"], b["recs"], inbuf, b["out_bytes"])
+    assert np.array_equal(tags_g, tags_u) and np.array_equal(out_g, out_u)
+    sample = rng.choice(n, 2000, replace=False)
+    out_o, tags_o = _oracle_seal(b["keys"], b["recs"][sample], inbuf, b["out_bytes"])
+    assert np.array_equal(tags_g.reshape(-1, 16)[sample], tags_o.reshape(-1, 16))
