@@ -306,14 +306,19 @@ class Engine:
 
     def _after_torch(self, *xs):
         """Device tensors from PyTorch: the engine's stream waits for the work already queued on
-        torch's current stream (e.g. the fill of a fresh torch.zeros output), without a host sync."""
+        torch's current stream (e.g. the fill of a fresh torch.zeros output), without a host sync.
+        The event and the engine-stream wrapper are made once per engine (a batch call then costs
+        one event record and one stream wait)."""
         for x in xs:
             if getattr(x, "is_cuda", False):
                 import torch
 
-                ev = torch.cuda.Event()
+                if getattr(self, "_torch_sync", None) is None or self._torch_sync[0] != x.device:
+                    self._torch_sync = (x.device, torch.cuda.Event(),
+                                        torch.cuda.ExternalStream(self.stream, device=x.device))
+                _, ev, ext = self._torch_sync
                 ev.record(torch.cuda.current_stream(x.device))
-                torch.cuda.ExternalStream(self.stream, device=x.device).wait_event(ev)
+                ext.wait_event(ev)
                 return
 
     def seal_batch(self, recs, inp, aux, out, tags, flags=0, n=None):

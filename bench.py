@@ -220,8 +220,12 @@ def main():
     flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
 
+    # raw device pointers: the buffers are resident and synchronized above, so no per-step wait
+    # on torch's stream is needed (Engine._after_torch)
+    p_recs, p_in, p_aux, p_out, p_tags = (t.data_ptr() for t in (d_recs, d_in, d_aux, d_out, d_tags))
+
     def step():
-        eng.seal_batch(d_recs.data_ptr(), d_in, d_aux, d_out, d_tags, flags=flags, n=n)
+        eng.seal_batch(p_recs, p_in, p_aux, p_out, p_tags, flags=flags, n=n)
 
     def sync():
         eng.sync()
