@@ -37,6 +37,10 @@ namespace atls {
 #define ATLS_CTR_CACHE 1
 #endif
 
+#ifndef ATLS_PREFETCH
+#define ATLS_PREFETCH 1  // fast steps load the next step's data block before their own AES rounds
+#endif
+
 #ifndef ATLS_DBG_SHARED_GHASH
 #define ATLS_DBG_SHARED_GHASH 0  // timing experiment only (wrong tags): one GHASH table per workgroup,
                                  // 16 waves per CU, to price the residency a per-key table would buy
@@ -315,13 +319,24 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 #pragma unroll
   for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e_comb - 1][w];
 
+  // Software pipelining (ATLS_PREFETCH): a fast step issues the load of the next step's block
+  // (1 KiB further) before its own AES rounds, so the HBM latency hides under a whole step instead
+  // of the last rounds; `pref` (wave-uniform) says Pn holds this step's block.
+  uint4 Pn = make_uint4(0u, 0u, 0u, 0u);
+  bool pref = false;
+  const uint32_t lim = min(in_bytes, n_aead);
   TT_STAMP(t_setup);
   for (uint32_t base = 0; base < S; base += 64) {
     TT_STAMP(t_step);
     const uint32_t s = base + (uint32_t)lane;
     if (base >= 64u && base + 64u <= fast_end) {  // wave-uniform
       const uint32_t off = (s - 1u - na) * 16u;
-      const uint4 Pu = ld16(src + off);
+      const uint4 Pu = pref ? Pn : ld16(src + off);
+      if (ATLS_PREFETCH) {  // every lane of a fast next step holds a whole block (fast_end)
+        const uint32_t offn = off + 1024u;
+        pref = base + 128u <= fast_end;
+        if (offn + 16u <= lim) Pn = ld16(src + offn);
+      }
       const v4u32 P = {Pu.x, Pu.y, Pu.z, Pu.w};
       uint32_t st[4];
       if (use_cache) {
@@ -348,6 +363,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 #endif
       continue;
     }
+    pref = false;
     if (ATLS_DBG_SKIP & 2) continue;
     if ((ATLS_DBG_SKIP & 16) && base + 64u >= S) continue;
     if ((ATLS_DBG_SKIP & 32) && base == 0u) continue;
@@ -620,6 +636,9 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
 #pragma unroll
   for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e_comb - 1][w];
 
+  uint4 Pn = make_uint4(0u, 0u, 0u, 0u);  // the next fast step's block (ATLS_PREFETCH, as gcm_record)
+  bool pref = false;
+  const uint32_t lim = min(len, n_aead);
   for (uint32_t t = 0; t < steps; t++) {
     const uint32_t base = t * (uint32_t)G;
     if ((base & 255u) == 0u) {  // a new ctr >> 8 (the same for every slot of the step): its cache words
@@ -634,7 +653,12 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
     const bool fast = base >= (uint32_t)G && base + G <= fast_end;
     if (__builtin_amdgcn_ballot_w64(!fast) == 0) {  // every group: whole data blocks only
       const uint32_t off = (s - 2u) * 16u;
-      const uint4 Pu = ld16(src + off);
+      const uint4 Pu = pref ? Pn : ld16(src + off);
+      if (ATLS_PREFETCH) {
+        const uint32_t offn = off + 16u * G;
+        if (offn + 16u <= lim) Pn = ld16(src + offn);
+        pref = true;  // used only if the next step is fast, and then every lane's load was in range
+      }
       uint32_t st[4];
       aes_ctr_r12(st, gl_addr ^ (((base & 0xffu) ^ k15) << 8), cur, lb);  // ctr = s
       aes_rounds_tt<NR, 3>(st, rk, rkr, lb);
@@ -650,6 +674,7 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
       continue;
     }
     // general step: slot 0 = E_K(J0), slot 1 = AAD, slots 2..m-1 data, slot m = length block
+    pref = false;
     const bool data = s >= 2u && s + 1u <= m;
     uint32_t P[4] = {0, 0, 0, 0};
     if (data) {

@@ -27,6 +27,11 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, unsigned long long* clk,
         if (OP == 8) { uint64_t t; asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(t) : "v"(a[i]), "v"(b)); a[i] = (uint32_t)t ^ (uint32_t)(t >> 32); }
         if (OP == 9) asm volatile("v_bfe_i32 %0, %0, %1, 1" : "+v"(a[i]) : "v"(b));
         if (OP == 10) asm volatile("v_lshrrev_b64 %0, 3, %0" : "+v"(*(uint64_t*)&a[i & ~1]));
+        if (OP == 11) asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a[i]) : "v"(b));
+        if (OP == 12) asm volatile("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:BYTE_1" : "+v"(a[i]) : "v"(b));
+        if (OP == 13) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
+        if (OP == 14) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(a[i]) : "v"(b));
+        if (OP == 15) asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PRESERVE src0_sel:DWORD src1_sel:WORD_1" : "+v"(a[i]) : "v"(b));
         if (OP == 4) { if (i & 1) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[i]) : "v"(b));
                        else asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[i]) : "v"(b), "v"(c)); }
       }
@@ -72,6 +77,11 @@ int main() {
     run<8>("mad_u64_u32", dout, dclk, w);
     run<9>("bfe_i32", dout, dclk, w);
     run<10>("lshr_b64", dout, dclk, w);
+    run<11>("mov_sdwa", dout, dclk, w);
+    run<12>("lshl_sdwa", dout, dclk, w);
+    run<13>("and_or", dout, dclk, w);
+    run<14>("lshl_or", dout, dclk, w);
+    run<15>("xor_sdwa", dout, dclk, w);
   }
   return 0;
 }
