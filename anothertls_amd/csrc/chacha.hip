@@ -433,6 +433,13 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 #ifndef ATLS_CHACHA_MINW_OPEN
 #define ATLS_CHACHA_MINW_OPEN 3  // 169 -> 168 VGPRs: 3 open waves per SIMD instead of 2 (C3 open 0.113 -> 0.106 ms)
 #endif
+// Planned (mixed-suite) batches run the ChaCha kernel beside the AES-GCM kernel, whose workgroup
+// holds 3 waves x 128 VGPRs per SIMD: at <= 128 VGPRs a ChaCha wave still fits next to it, so the
+// LDS-bound and the VALU-bound kernel share every CU (C5 658-670 -> 705-712 GiB/s, same-box A/B;
+// the direct C3 batch loses 19 % at that register cap and keeps the bounds above).
+#ifndef ATLS_CHACHA_MINW_SIDE
+#define ATLS_CHACHA_MINW_SIDE 4
+#endif
 template <bool OPEN, int G>
 __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
   const WorkList W{A.idx, A.plan, kListChacha, A.n};
@@ -465,10 +472,10 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
   }
 }
 
-template <bool OPEN>
-__global__ __launch_bounds__(256, OPEN ? ATLS_CHACHA_MINW_OPEN : ATLS_CHACHA_MINW_SEAL) void chacha_kernel(ChArgs A) {
+template <bool OPEN, bool PLANNED>
+__global__ __launch_bounds__(256, PLANNED ? ATLS_CHACHA_MINW_SIDE : OPEN ? ATLS_CHACHA_MINW_OPEN : ATLS_CHACHA_MINW_SEAL) void chacha_kernel(ChArgs A) {
   const int lane = threadIdx.x & 63;
-  if (A.idx) chacha_batch<OPEN, 16>(A, lane);
+  if constexpr (PLANNED) chacha_batch<OPEN, 16>(A, lane);
   else chacha_direct<OPEN>(A, lane);
 }
 
@@ -486,7 +493,12 @@ extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs
   // strides over 16 positions per wave and simply finishes its list sooner
   const uint32_t want16 = (n + 15u) / 16u;
   const uint32_t g = (uint32_t)grid < want16 ? (uint32_t)grid : want16;
-  if (open) hipLaunchKernelGGL((atls::chacha_kernel<true>), dim3(g), dim3(256), 0, s, A);
-  else hipLaunchKernelGGL((atls::chacha_kernel<false>), dim3(g), dim3(256), 0, s, A);
+  if (idx) {
+    if (open) hipLaunchKernelGGL((atls::chacha_kernel<true, true>), dim3(g), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((atls::chacha_kernel<false, true>), dim3(g), dim3(256), 0, s, A);
+  } else {
+    if (open) hipLaunchKernelGGL((atls::chacha_kernel<true, false>), dim3(g), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((atls::chacha_kernel<false, false>), dim3(g), dim3(256), 0, s, A);
+  }
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }

@@ -41,6 +41,13 @@ namespace atls {
 #define ATLS_PREFETCH 1  // fast steps load the next step's data block before their own AES rounds
 #endif
 
+#ifndef ATLS_GCM_DOUBLE
+#define ATLS_GCM_DOUBLE 12  // lane groups of keys with >= this many rounds: two fast steps per pass, their
+                            // AES rounds software-pipelined (aes_rounds_tt2). Same-box A/B
+                            // (profiles/r02/ab_double.log): C4 780 -> 795 GiB/s, C2 883 -> 862 (so AES-128
+                            // keeps single steps); 99 = off
+#endif
+
 #ifndef ATLS_DBG_SHARED_GHASH
 #define ATLS_DBG_SHARED_GHASH 0  // timing experiment only (wrong tags): one GHASH table per workgroup,
                                  // 16 waves per CU, to price the residency a per-key table would buy
@@ -115,6 +122,66 @@ __device__ __forceinline__ void aes_rounds_tt(uint32_t (&s)[4], const uint32_t* 
   } else {
     tt_final(s, rk + 4 * NR, lb);
   }
+}
+
+// A prefetch address: the block at `want` if it lies within the first `lim` bytes, else this
+// step's own block `cur` (loaded again, unused). The load is issued by every lane either way: a
+// lane-predicated load would make the compiler's counter wait for the prefetches of this step
+// too (s_waitcnt vmcnt(0)) before it may use the blocks prefetched for it.
+__device__ __forceinline__ uint32_t pf_off(uint32_t want, uint32_t cur, uint32_t lim) {
+  return want + 16u <= lim ? want : cur;
+}
+
+// Two independent blocks through rounds R0 .. NR as a two-stage software pipeline: a round's 16
+// lookups of one block are issued, then the other block's XORs of its previous round (and its
+// next lookups) run while they are in flight. sched_barrier keeps the stages in this order, so a
+// wave keeps 16 lookups in flight while it computes (one block per lane leaves it none).
+// Lookups of one round of one block, as tt_round (FIN: as tt_final, T0 for a / bb, T1 for cc / dd).
+__device__ __forceinline__ void tt_look(const uint32_t (&s)[4], uint32_t lb, bool fin, uint32_t (&L)[16]) {
+  const uint32_t s0 = s[0], s1 = s[1], s2 = s[2], s3 = s[3];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t a = (c == 0 ? s0 : c == 1 ? s1 : c == 2 ? s2 : s3);
+    const uint32_t bb = (c == 0 ? s1 : c == 1 ? s2 : c == 2 ? s3 : s0);
+    const uint32_t cc = (c == 0 ? s2 : c == 1 ? s3 : c == 2 ? s0 : s1);
+    const uint32_t dd = (c == 0 ? s3 : c == 1 ? s0 : c == 2 ? s1 : s2);
+    L[4 * c] = lds_u32(TA(cc, 16) + (fin ? 128u : 0u));
+    L[4 * c + 1] = lds_u32(TA(dd, 24) + 128);
+    L[4 * c + 2] = lds_u32(TA(a, 0));
+    L[4 * c + 3] = lds_u32(TA(bb, 8) + (fin ? 0u : 128u));
+  }
+}
+__device__ __forceinline__ void tt_comb(uint32_t (&s)[4], const uint32_t (&L)[16], const uint32_t* kr) {
+#pragma unroll
+  for (int c = 0; c < 4; c++) s[c] = xor3(L[4 * c + 2], L[4 * c + 3], rot16(xor3(L[4 * c], L[4 * c + 1], kr[c])));
+}
+__device__ __forceinline__ void tt_comb_final(uint32_t (&s)[4], const uint32_t (&L)[16], const uint32_t* kf) {
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const uint32_t lo = perm(L[4 * c + 3], L[4 * c + 2], 0x0c0c0501u);
+    const uint32_t hi = perm(L[4 * c + 1], L[4 * c], 0x07020c0cu);
+    s[c] = __builtin_amdgcn_bitop3_b32(lo, hi, kf[c], 0x56);
+  }
+}
+template <int NR, int R0>
+__device__ __forceinline__ void aes_rounds_tt2(uint32_t (&a)[4], uint32_t (&b)[4], const uint32_t* rk, const uint32_t* rkr,
+                                               uint32_t lb) {
+  uint32_t La[16], Lb[16];
+  tt_look(a, lb, R0 == NR, La);
+  __builtin_amdgcn_sched_barrier(0);
+  tt_look(b, lb, R0 == NR, Lb);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int r = R0; r < NR; r++) {
+    tt_comb(a, La, rkr + 4 * r);
+    tt_look(a, lb, r + 1 == NR, La);
+    __builtin_amdgcn_sched_barrier(0);
+    tt_comb(b, Lb, rkr + 4 * r);
+    tt_look(b, lb, r + 1 == NR, Lb);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  tt_comb_final(a, La, rk + 4 * NR);
+  tt_comb_final(b, Lb, rk + 4 * NR);
 }
 
 template <int NR>
@@ -335,7 +402,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       if (ATLS_PREFETCH) {  // every lane of a fast next step holds a whole block (fast_end)
         const uint32_t offn = off + 1024u;
         pref = base + 128u <= fast_end;
-        if (offn + 16u <= lim) Pn = ld16(src + offn);
+        Pn = ld16(src + (offn + 16u <= lim ? offn : off));  // always issued (see pf_off)
       }
       const v4u32 P = {Pu.x, Pu.y, Pu.z, Pu.w};
       uint32_t st[4];
@@ -636,7 +703,8 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
 #pragma unroll
   for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e_comb - 1][w];
 
-  uint4 Pn = make_uint4(0u, 0u, 0u, 0u);  // the next fast step's block (ATLS_PREFETCH, as gcm_record)
+  // ATLS_PREFETCH as in gcm_record: Pn / Pn2 hold the blocks of the next one or two fast steps
+  uint4 Pn = make_uint4(0u, 0u, 0u, 0u), Pn2 = make_uint4(0u, 0u, 0u, 0u);
   bool pref = false;
   const uint32_t lim = min(len, n_aead);
   for (uint32_t t = 0; t < steps; t++) {
@@ -654,9 +722,43 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
     if (__builtin_amdgcn_ballot_w64(!fast) == 0) {  // every group: whole data blocks only
       const uint32_t off = (s - 2u) * 16u;
       const uint4 Pu = pref ? Pn : ld16(src + off);
+      // ATLS_GCM_DOUBLE: the next step is fast too and shares this step's counter-cache words
+      const bool dbl = NR >= ATLS_GCM_DOUBLE && ((base + G) & 255u) != 0u &&
+                       __builtin_amdgcn_ballot_w64(!(base + 2u * G <= fast_end)) == 0;
+      if (dbl) {
+        const uint32_t off2 = off + 16u * G;
+        const uint4 Pv = pref ? Pn2 : ld16(src + off2);
+        if (ATLS_PREFETCH) {  // the blocks of steps t + 2 and t + 3 (used only if those are fast)
+          Pn = ld16(src + pf_off(off2 + 16u * G, off, lim));
+          Pn2 = ld16(src + pf_off(off2 + 32u * G, off, lim));
+          pref = true;
+        }
+        uint32_t sa[4], sb[4];
+        aes_ctr_r12(sa, gl_addr ^ (((base & 0xffu) ^ k15) << 8), cur, lb);  // ctr = s
+        aes_ctr_r12(sb, gl_addr ^ ((((base + G) & 0xffu) ^ k15) << 8), cur, lb);  // ctr = s + G
+        aes_rounds_tt2<NR, 3>(sa, sb, rk, rkr, lb);
+        const uint32_t C[4] = {Pu.x ^ sa[0], Pu.y ^ sa[1], Pu.z ^ sa[2], Pu.w ^ sa[3]};
+        const uint32_t D[4] = {Pv.x ^ sb[0], Pv.y ^ sb[1], Pv.z ^ sb[2], Pv.w ^ sb[3]};
+        st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
+        st16(dst + off2, make_uint4(D[0], D[1], D[2], D[3]));
+        if (OPEN) {  // the later block's last non-zero byte wins
+          const int j = last_nonzero(C, 16), j2 = last_nonzero(D, 16);
+          if (j2 >= 0) lastnz = ((int64_t)(off2 + j2) << 8) | ((D[j2 >> 2] >> (8 * (j2 & 3))) & 0xffu);
+          else if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((C[j >> 2] >> (8 * (j & 3))) & 0xffu);
+        }
+        ghash_mul<ATLS_GHASH_W>(y, wb);
+        if (OPEN) { y[0] ^= Pu.x; y[1] ^= Pu.y; y[2] ^= Pu.z; y[3] ^= Pu.w; }
+        else { y[0] ^= C[0]; y[1] ^= C[1]; y[2] ^= C[2]; y[3] ^= C[3]; }
+        ghash_mul<ATLS_GHASH_W>(y, wb);
+        if (OPEN) { y[0] ^= Pv.x; y[1] ^= Pv.y; y[2] ^= Pv.z; y[3] ^= Pv.w; }
+        else { y[0] ^= D[0]; y[1] ^= D[1]; y[2] ^= D[2]; y[3] ^= D[3]; }
+        t++;
+        continue;
+      }
       if (ATLS_PREFETCH) {
         const uint32_t offn = off + 16u * G;
-        if (offn + 16u <= lim) Pn = ld16(src + offn);
+        Pn = ld16(src + pf_off(offn, off, lim));
+        Pn2 = ld16(src + pf_off(offn + 16u * G, off, lim));
         pref = true;  // used only if the next step is fast, and then every lane's load was in range
       }
       uint32_t st[4];
