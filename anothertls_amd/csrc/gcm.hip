@@ -597,6 +597,9 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 #endif
 // 8 lanes measured faster for AES-128 (C2 854 -> 873 GiB/s) and slower for AES-256 (C4 790 ->
 // 745), same-box A/B (profiles/r02/ab_gcm_group_variants.log)
+#ifndef ATLS_GROUP_TAIL
+#define ATLS_GROUP_TAIL 4  // the last (TAIL / 4) x (waves in the grid) grouped records run as single records
+#endif
 #ifndef ATLS_GROUP_SHARES
 #define ATLS_GROUP_SHARES 1  // work counters of a grouped batch (1..8): shares of region A by blockIdx % shares
                              // (8 measured no faster than 1: C2 850 vs 857 GiB/s, same-box A/B)
@@ -909,8 +912,12 @@ __device__ __forceinline__ void gcm_one(const GcmArgs& A, uint32_t r, uint32_t l
 template <bool OPEN, int kWaves, int NR>
 __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  // T0 (1 KiB) through the (still unused) GHASH area: one global load per thread instead of a
+  // dependent load per LDS word of the 64 KiB replicated tables
+  if (threadIdx.x < 256) smem[kTabBytes / 4 + threadIdx.x] = A.t0[threadIdx.x];
+  __syncthreads();
   for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
-    const uint32_t v = A.t0[i >> 6];
+    const uint32_t v = smem[kTabBytes / 4 + (i >> 6)];
     smem[i] = (i & 32) ? rotl32(v, 8) : v;  // row x: T0[x] x32 | T1[x] x32
   }
   __syncthreads();
@@ -946,7 +953,7 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   const uint32_t x = blockIdx.x % nx;
   const uint32_t nq = n_a / NG;  // runs (n_a is a multiple of kGroupRun)
   const uint32_t q0 = (uint32_t)((uint64_t)nq * x / nx), sq = (uint32_t)((uint64_t)nq * (x + 1u) / nx) - q0;
-  const uint32_t tail_q = stride / nx / NG;
+  const uint32_t tail_q = stride * ATLS_GROUP_TAIL / (4u * nx * NG);
   const uint32_t nrun = sq > tail_q ? sq - tail_q : 0u;
   const uint32_t n_units = nrun + NG * (sq - nrun);
   if (n_units == 0) return;
