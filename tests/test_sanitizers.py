@@ -6,6 +6,7 @@ sanitizers"; GPU sanitizers are not available on this pool):
   mirror of the reference's Record::from_raw (anothertls_amd/record.py, net/record.rs:81-102);
 * the oracle (oracle/ref_restatement.c) over every entry point (tests/native/oracle_asan.c).
 """
+import fcntl
 import os
 import random
 import struct
@@ -22,10 +23,15 @@ NATIVE = os.path.join(ROOT, "tests", "native")
 
 @pytest.fixture(scope="module")
 def san_build():
-    try:
-        subprocess.check_call(["make", "-s", "-C", NATIVE, "san"])
-    except (OSError, subprocess.CalledProcessError) as exc:  # no sanitizer runtime in this toolchain
-        pytest.skip(f"sanitizer build unavailable: {exc}")
+    # one build at a time: pytest-xdist workers each run this fixture, and a second `make`
+    # rewriting a binary the first worker is executing fails with ETXTBSY
+    os.makedirs(os.path.join(NATIVE, "build"), exist_ok=True)
+    with open(os.path.join(NATIVE, "build", ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            subprocess.check_call(["make", "-s", "-C", NATIVE, "san"])
+        except (OSError, subprocess.CalledProcessError) as exc:  # no sanitizer runtime here
+            pytest.skip(f"sanitizer build unavailable: {exc}")
     return os.path.join(NATIVE, "build")
 
 
