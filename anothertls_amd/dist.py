@@ -141,6 +141,38 @@ def seal_sharded(seal, recs, inp=None, out=None, tags=None, device=None):
     return a, b
 
 
+def run_or_exit(fn, timeout_s, on_timeout):
+    """fn() with a watchdog: if it has not returned after timeout_s seconds, on_timeout() runs
+    (e.g. print the result gathered so far) and the process exits with status 0 -- for steps
+    after a benchmark's timed region whose collectives could hang (a hung rank must not cost the
+    measured line). Returns (True, fn's value) or (False, the exception fn raised)."""
+    import threading
+
+    lock, state = threading.Lock(), {"done": False}
+
+    def fire():
+        with lock:
+            if state["done"]:
+                return
+            state["done"] = True
+            try:
+                on_timeout()
+            finally:
+                os._exit(0)
+
+    timer = threading.Timer(timeout_s, fire)
+    timer.daemon = True
+    timer.start()
+    try:
+        res = (True, fn())
+    except Exception as exc:  # noqa: BLE001 -- reported to the caller
+        res = (False, exc)
+    with lock:
+        state["done"] = True
+        timer.cancel()
+    return res
+
+
 def close():
     if tdist.is_available() and tdist.is_initialized():
         barrier()

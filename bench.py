@@ -58,6 +58,8 @@ def parse():
                    help="also time the same records sealed as one wire stream (ATLS_MODE_WIRE)")
     p.add_argument("--no-scatter", action="store_true",
                    help="N > 1: skip the sharded scatter / seal / gather of rank 0's batch")
+    p.add_argument("--scatter-timeout", type=float, default=120.0,
+                   help="N > 1: seconds the sharded exchange may take before the line is printed without it")
     return p.parse_args()
 
 
@@ -329,12 +331,21 @@ def main():
         # over all ranks, scattered over RCCL, sealed by every rank's engine and gathered back
         # (dist.seal_sharded); reported beside `value`, which is the pre-sharded rate. The result
         # must equal rank 0's own single-GPU seal of the same records (d_out / d_tags above).
-        try:
-            sg = sharded_exchange(args, eng, dev, d_in if rank == 0 else None, d_aux, d_out if rank == 0 else None,
-                                  d_tags if rank == 0 else None)
-        except Exception as exc:  # the bench line must survive a collective failure
-            sg = None
-            print(f"sharded exchange failed: {exc}", file=sys.stderr, flush=True)
+        # The bench line must survive a failed or hung exchange: errors are caught, and a
+        # watchdog on every rank ends the process after --scatter-timeout s, rank 0 first
+        # printing the line without the exchange.
+        def give_up():
+            if rank == 0 and result is not None:
+                result["sharded_from_rank0"] = {"error": f"no result within {args.scatter_timeout:.0f} s"}
+                print(json.dumps(result), flush=True)
+
+        ok, sg = dist.run_or_exit(
+            lambda: sharded_exchange(args, eng, dev, d_in if rank == 0 else None, d_aux,
+                                     d_out if rank == 0 else None, d_tags if rank == 0 else None),
+            args.scatter_timeout, give_up)
+        if not ok:  # the bench line must survive a collective failure
+            print(f"sharded exchange failed: {sg}", file=sys.stderr, flush=True)
+            sg = {"error": str(sg)[:200]}
         if rank == 0 and result is not None:
             result["sharded_from_rank0"] = sg
     if rank == 0:

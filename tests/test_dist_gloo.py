@@ -116,3 +116,23 @@ def test_partition_balances_cumulative_bytes():
     # more parts than records: empty parts, still a tiling
     f = atls.partition(b["recs"][:3], 8)
     assert f[0] == 0 and f[-1] == 3 and (np.diff(f) >= 0).all()
+
+
+def test_run_or_exit_watchdog():
+    """bench.py's guard around the post-timing exchange (dist.run_or_exit): a step that returns
+    or raises is reported; one that hangs ends the process after the timeout, status 0, once the
+    timeout callback (bench.py: print the bench line) has run."""
+    import subprocess
+
+    code = (
+        "import sys, time; sys.path.insert(0, %r)\n"
+        "from anothertls_amd import dist\n"
+        "print(dist.run_or_exit(lambda: 7, 5, lambda: print('LATE')))\n"
+        "ok, exc = dist.run_or_exit(lambda: 1 / 0, 5, lambda: print('LATE'))\n"
+        "print(ok, type(exc).__name__)\n"
+        "dist.run_or_exit(lambda: time.sleep(60), 0.5, lambda: print('LINE', flush=True))\n"
+        "print('NOT REACHED')\n" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.split("\n")[:3] == ["(True, 7)", "False ZeroDivisionError", "LINE"], r.stdout
+    assert "NOT REACHED" not in r.stdout and "LATE" not in r.stdout
