@@ -5,7 +5,7 @@
 // the last 64-byte block unencrypted when len % 64 == 0 (cipher.rs:99-102), and the tag is
 // computed over that output. Record framing as in net/record.rs:162-240.
 //
-// Mapping: a group of G lanes per record (G = 16, or 4 for short records, chacha_kernel). Slot j of a record
+// Mapping: a group of G lanes per record (G = 16; 4 or 2 for short records, chacha_kernel). Slot j of a record
 // is ChaCha20 block counter j: slot 0 = Poly1305 key generation (poly1305.rs:19-22) plus the
 // AAD blocks, slot j >= 1 = bytes [64(j-1), 64j) of the record (counter starts at 1,
 // poly1305.rs:77). Lane l of the group owns slots j = l (mod 16): each step the group reads and
@@ -418,9 +418,10 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 // G = 4 (batches whose records are all short, ATLS_CHACHA_SHORT): 16 positions per wave and step,
 // one per 4-lane group: the per-record Poly1305 set-up (r powers, lane scan, combine) is shared
 // by 4 lanes instead of 16, and a 1.5 KiB record's 26 ChaCha blocks fill 28 lane-slots instead
-// of 32 (C3: 690 -> 906 GiB/s). Direct batches: a wave takes 16 consecutive positions per step
-// and picks the width from their longest record -- 4 lanes each if all are short, else 16 lanes
-// in four rounds of 4 records -- so no pass over the batch precedes the launch (an earlier version ran a
+// of 32 (C3: 690 -> 906 GiB/s). Direct batches: a wave takes 32 consecutive positions per step
+// and picks the width from their longest record -- 2 lanes each if all are tiny (ATLS_CHACHA_TINY),
+// 4 lanes in two rounds of 16 records if all are short, else 16 lanes in eight rounds of 4 records
+// -- so no pass over the batch precedes the launch (an earlier version ran a
 // batch_prep kernel for the batch's longest record and launched one kernel per width: two extra
 // dispatches, ≈10 µs of every C3 batch). Planned batches (mixed lengths, longest first) run
 // G = 16, 4 positions per wave and step, keeping the fine round-robin the longest-first order
@@ -428,7 +429,8 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 // Minimum waves per SIMD of the seal / open kernels (__launch_bounds__): caps their VGPRs
 // (3 -> 168, 4 -> 128), i.e. how many waves of each a SIMD holds.
 #ifndef ATLS_CHACHA_MINW_SEAL
-#define ATLS_CHACHA_MINW_SEAL 1
+#define ATLS_CHACHA_MINW_SEAL 3  // the 2-lane path took the seal kernel to 171 VGPRs (2 waves per SIMD); capped
+                                 // at 168 (1 spill): C3 0.0868 -> 0.0864 ms (profiles/r02/ab_chacha_tiny.log)
 #endif
 #ifndef ATLS_CHACHA_MINW_OPEN
 #define ATLS_CHACHA_MINW_OPEN 3  // 169 -> 168 VGPRs: 3 open waves per SIMD instead of 2 (C3 open 0.113 -> 0.106 ms)
@@ -451,23 +453,43 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
     chacha_group<OPEN, G>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
 }
 
-// Direct batch: 16 positions per wave and step, the width chosen per step from their longest record.
+// Records up to ATLS_CHACHA_TINY bytes (every record of a wave step) take ATLS_CHACHA_TINY_G
+// lanes each: a direct batch's wave step then covers 64 / TINY_G positions (0: off, 16 per step).
+// At 2 lanes an MTU-sized record's Poly1305 set-up (r powers, a one-level lane scan, combine) is
+// shared by 2 lanes instead of 4 and its 26 ChaCha blocks fill 26 lane-slots instead of 28; a
+// 64 Ki-record batch still gives 2 waves per SIMD. Same-box A/B, 3 rounds
+// (profiles/r02/ab_chacha_tiny.log): C3 seal kernel 0.0895 ms (4 lanes) -> 0.0864 ms (2 lanes,
+// -3.5 %); 1 lane per record (one wave per SIMD) 0.0982 ms; opens and C5 unchanged.
+#ifndef ATLS_CHACHA_TINY
+#define ATLS_CHACHA_TINY 2048
+#endif
+#ifndef ATLS_CHACHA_TINY_G
+#define ATLS_CHACHA_TINY_G 2
+#endif
+
+// Direct batch: P positions per wave and step, the width chosen per step from their longest record.
 template <bool OPEN>
 __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
   const WorkList W{nullptr, nullptr, kListChacha, A.n};
   const uint32_t cnt = A.n;
+  constexpr uint32_t P = ATLS_CHACHA_TINY ? 64u / ATLS_CHACHA_TINY_G : 16u;
+  static_assert(P >= 16 && P <= 64, "a wave step covers 16 to 64 positions");
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
-  const uint32_t stride = gridDim.x * blockDim.x / 64u * 16u;
-  for (uint32_t q0 = wave * 16u; q0 < cnt; q0 += stride) {
-    uint32_t mx = (lane < 16 && q0 + (uint32_t)lane < cnt) ? A.recs[q0 + (uint32_t)lane].len : 0u;
+  const uint32_t stride = gridDim.x * blockDim.x / 64u * P;
+  for (uint32_t q0 = wave * P; q0 < cnt; q0 += stride) {
+    uint32_t mx = ((uint32_t)lane < P && q0 + (uint32_t)lane < cnt) ? A.recs[q0 + (uint32_t)lane].len : 0u;
 #pragma unroll
-    for (int off = 8; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    for (int off = (int)P / 2; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
     mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
-    if (mx <= (uint32_t)ATLS_CHACHA_SHORT) {
-      chacha_group<OPEN, 4>(A, W, q0 + (uint32_t)lane / 4u, cnt, lane & 3);
+    if (ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY) {
+      constexpr int G = ATLS_CHACHA_TINY ? ATLS_CHACHA_TINY_G : 4;
+      chacha_group<OPEN, G>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
+    } else if (mx <= (uint32_t)ATLS_CHACHA_SHORT) {
+#pragma unroll 1
+      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3);
     } else {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < 4u; rr++) chacha_group<OPEN, 16>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15);
+      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15);
     }
   }
 }

@@ -1,7 +1,8 @@
-"""GPU: the two ChaCha20-Poly1305 lane widths (chacha.hip). In a direct batch each wave takes 16
-consecutive records and runs them 4 lanes per record when all are short (<= ATLS_CHACHA_SHORT =
-4096 B), else 16 lanes per record in four rounds (the second case below puts one long record among
-short ones, so both widths run in one launch); both are
+"""GPU: the three ChaCha20-Poly1305 lane widths (chacha.hip). In a direct batch each wave takes 32
+consecutive records and runs them 2 lanes per record when all are tiny (<= ATLS_CHACHA_TINY = 2048
+B), else 4 lanes per record in two rounds when all are short (<= ATLS_CHACHA_SHORT = 4096 B), else
+16 lanes per record in eight rounds (the third case below puts one long record among short ones,
+so two widths run in one launch); all are
 checked against the oracle on the lengths that exercise the per-lane Poly1305 combine and the
 reference's F4 quirk (ChaCha20::encrypt leaves the last block unencrypted when len % 64 == 0,
 crypto/chacha20/cipher.rs:99-102), sealed and reopened, with tampered tags."""
@@ -13,6 +14,7 @@ import oracle as ora
 pytestmark = pytest.mark.gpu
 
 SHORT = [0, 1, 15, 16, 17, 62, 63, 64, 65, 127, 128, 191, 255, 256, 1000, 1023, 1024, 1535, 1536, 2047, 4095, 4096]
+TINY = [n for n in SHORT if n < 2048]
 
 
 @pytest.fixture(scope="module")
@@ -24,7 +26,8 @@ def atls():
     return a
 
 
-@pytest.mark.parametrize("lens", [SHORT * 20, SHORT * 20 + [16384]], ids=["all-short-4-lanes", "one-long-16-lanes"])
+@pytest.mark.parametrize("lens", [TINY * 20, SHORT * 20, SHORT * 20 + [16384]],
+                         ids=["all-tiny-2-lanes", "all-short-4-lanes", "one-long-16-lanes"])
 def test_chacha_widths_vs_oracle(atls, lens):
     from anothertls_amd import workload
 
