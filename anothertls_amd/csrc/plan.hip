@@ -1,4 +1,4 @@
-// Batch plan: three small launches before the record kernels.
+// Batch plan: two small launches before the record kernels.
 //
 //  1. plan_count: classifies every record (validation of net/record.rs-style descriptors against
 //     the key table, crypto/ciphersuite.rs:78-87 get_cipher: AES-GCM for 0x1301/0x1302 with the
@@ -6,9 +6,10 @@
 //     into a work list -- AES-GCM with 10 / 12 / 14 rounds, ChaCha20-Poly1305 -- and a length
 //     class; rejected records get their status here (err flag; open results for open batches).
 //     Each workgroup counts its chunk of the batch in an LDS histogram.
-//  2. plan_scan: one workgroup turns the per-workgroup histograms into offsets, lists in order,
-//     classes longest record first.
-//  3. plan_scatter: each workgroup writes its records' indices at its offsets (LDS cursors).
+//  2. plan_scatter: each workgroup turns the per-workgroup histograms into its own offsets (lists
+//     in order, classes longest record first) and writes its records' indices there (LDS
+//     cursors). (A separate one-workgroup plan_scan launch did the offsets before: 14.5 us of a
+//     C5 batch; ATLS_PLAN_FUSED_SCAN=0 restores it.)
 //
 // The record kernels (gcm.hip, chacha.hip) take their list's positions round-robin (WorkList,
 // plan.h), so every worker gets a similar mix of lengths (LPT-like balance for the
@@ -119,9 +120,52 @@ __global__ __launch_bounds__(1024) void plan_scan(const uint32_t* wgcount, uint3
   if (t == blockDim.x - 1u) P->off[kPlanLists] = part[t];
 }
 
-__global__ __launch_bounds__(256) void plan_scatter(uint32_t n, const uint8_t* keys, const uint32_t* wgoff, uint32_t* idx) {
+#ifndef ATLS_PLAN_FUSED_SCAN
+#define ATLS_PLAN_FUSED_SCAN 1
+#endif
+// wgoff == nullptr (ATLS_PLAN_FUSED_SCAN): no plan_scan launch; every workgroup derives its own
+// start offsets from the G x 64 histograms -- per key the total over all workgroups and the part
+// of the workgroups before it (4 threads per key), then an exclusive scan of the 64 totals in one
+// wave -- and workgroup 0 writes the list offsets. G x 64 words are read by every workgroup (32 KiB
+// at G = 128, from L2) instead of one 1,024-thread workgroup scanning them between two launches.
+__global__ __launch_bounds__(256) void plan_scatter(uint32_t n, const uint8_t* keys, const uint32_t* wgoff,
+                                                    const uint32_t* wgcount, PlanHdr* P, uint32_t* idx) {
+  static_assert(kPlanKeys == 64, "one wave scans the key totals");
   __shared__ uint32_t cur[kPlanKeys];
-  for (uint32_t t = threadIdx.x; t < kPlanKeys; t += blockDim.x) cur[t] = wgoff[t * gridDim.x + blockIdx.x];
+  if (wgoff) {
+    for (uint32_t t = threadIdx.x; t < kPlanKeys; t += blockDim.x) cur[t] = wgoff[t * gridDim.x + blockIdx.x];
+  } else {
+    __shared__ uint32_t tot[kPlanKeys], pre[kPlanKeys];
+    const uint32_t G = gridDim.x, b = blockIdx.x, k = threadIdx.x >> 2, q = threadIdx.x & 3u;
+    uint32_t all = 0, before = 0;
+    if (k < kPlanKeys) {
+      const uint32_t* row = wgcount + k * G;
+#pragma unroll 8
+      for (uint32_t c = q; c < G; c += 4u) {
+        const uint32_t v = row[c];
+        all += v;
+        before += c < b ? v : 0u;
+      }
+    }
+    all += __shfl_xor(all, 1, 4); all += __shfl_xor(all, 2, 4);
+    before += __shfl_xor(before, 1, 4); before += __shfl_xor(before, 2, 4);
+    if (q == 0 && k < kPlanKeys) { tot[k] = all; pre[k] = before; }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const uint32_t v = tot[threadIdx.x];
+      uint32_t inc = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, (unsigned)d, 64);
+        if (threadIdx.x >= (uint32_t)d) inc += o;
+      }
+      cur[threadIdx.x] = inc - v + pre[threadIdx.x];
+      if (b == 0) {  // list l starts at its longest class, key l * kPlanClasses
+        if (threadIdx.x % kPlanClasses == 0) P->off[threadIdx.x / kPlanClasses] = inc - v;
+        if (threadIdx.x == 63) P->off[kPlanLists] = inc;
+      }
+    }
+  }
   __syncthreads();
   uint32_t lo, hi;
   plan_chunk(n, lo, hi);
@@ -248,7 +292,9 @@ extern "C" int atls_launch_plan(int open, const void* ks, const atls_rec* recs, 
   uint32_t* wgoff = wg + atls::kPlanKeys * atls::kPlanMaxWG;
   hipLaunchKernelGGL(atls::plan_count, dim3(G), dim3(256), 0, s, recs, n, (const atls::KeySched*)ks, n_slots,
                      (uint32_t)(open != 0), res, err, keys, wgcount);
-  hipLaunchKernelGGL(atls::plan_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)wgcount, G, wgoff, hdr);
-  hipLaunchKernelGGL(atls::plan_scatter, dim3(G), dim3(256), 0, s, n, (const uint8_t*)keys, (const uint32_t*)wgoff, idx);
+  if (!ATLS_PLAN_FUSED_SCAN)
+    hipLaunchKernelGGL(atls::plan_scan, dim3(1), dim3(1024), 0, s, (const uint32_t*)wgcount, G, wgoff, hdr);
+  hipLaunchKernelGGL(atls::plan_scatter, dim3(G), dim3(256), 0, s, n, (const uint8_t*)keys,
+                     ATLS_PLAN_FUSED_SCAN ? nullptr : (const uint32_t*)wgoff, (const uint32_t*)wgcount, hdr, idx);
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
