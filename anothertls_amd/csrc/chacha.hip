@@ -442,6 +442,10 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 #ifndef ATLS_CHACHA_MINW_SIDE
 #define ATLS_CHACHA_MINW_SIDE 4
 #endif
+#ifndef ATLS_CHACHA_PLANNED_G
+#define ATLS_CHACHA_PLANNED_G 16  // lanes per record in planned (mixed) batches; C5 0.341 ms at 16, 0.359 at
+                                  // 8, 0.435 at 4 (profiles/r02/ab_chacha_planned_g.log)
+#endif
 template <bool OPEN, int G>
 __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
   const WorkList W{A.idx, A.plan, kListChacha, A.n};
@@ -497,7 +501,7 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
 template <bool OPEN, bool PLANNED>
 __global__ __launch_bounds__(256, PLANNED ? ATLS_CHACHA_MINW_SIDE : OPEN ? ATLS_CHACHA_MINW_OPEN : ATLS_CHACHA_MINW_SEAL) void chacha_kernel(ChArgs A) {
   const int lane = threadIdx.x & 63;
-  if constexpr (PLANNED) chacha_batch<OPEN, 16>(A, lane);
+  if constexpr (PLANNED) chacha_batch<OPEN, ATLS_CHACHA_PLANNED_G>(A, lane);
   else chacha_direct<OPEN>(A, lane);
 }
 
