@@ -184,6 +184,28 @@ __device__ __forceinline__ void aes_rounds_tt2(uint32_t (&a)[4], uint32_t (&b)[4
   tt_comb_final(b, Lb, rk + 4 * NR);
 }
 
+#ifndef ATLS_TT_ISSUE_ALL
+#define ATLS_TT_ISSUE_ALL 1  // lane-group fast steps issue a round's 16 lookups before any of its XORs: C2 -0.4 to
+                             // -0.7 %, C4 -0.5 %, C5 -0.8 % kernel time over two same-box A/Bs of 3 rounds each
+                             // (profiles/r02/ab_issue16*.log); the same for one-record-per-wave steps and with
+                             // the GHASH lookups spread over the rounds measured no better
+#endif
+// Rounds R0 .. NR of one block, each round's 16 lookups issued before its XORs (tt_look / tt_comb).
+template <int NR, int R0>
+__device__ __forceinline__ void aes_rounds_tt1(uint32_t (&a)[4], const uint32_t* rk, const uint32_t* rkr, uint32_t lb) {
+  uint32_t L[16];
+#pragma unroll
+  for (int r = R0; r < NR; r++) {
+    tt_look(a, lb, false, L);
+    __builtin_amdgcn_sched_barrier(0);
+    tt_comb(a, L, rkr + 4 * r);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  tt_look(a, lb, true, L);
+  __builtin_amdgcn_sched_barrier(0);
+  tt_comb_final(a, L, rk + 4 * NR);
+}
+
 template <int NR>
 __device__ __forceinline__ void aes_encrypt_tt(uint32_t (&s)[4], const uint32_t* rk, const uint32_t* rkr,
                                                uint32_t lb) {
@@ -766,7 +788,8 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
       }
       uint32_t st[4];
       aes_ctr_r12(st, gl_addr ^ (((base & 0xffu) ^ k15) << 8), cur, lb);  // ctr = s
-      aes_rounds_tt<NR, 3>(st, rk, rkr, lb);
+      if (ATLS_TT_ISSUE_ALL) aes_rounds_tt1<NR, 3>(st, rk, rkr, lb);
+      else aes_rounds_tt<NR, 3>(st, rk, rkr, lb);
       const uint32_t C[4] = {Pu.x ^ st[0], Pu.y ^ st[1], Pu.z ^ st[2], Pu.w ^ st[3]};
       st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
       if (OPEN) {

@@ -12,7 +12,7 @@ done
 for round in 1 2 3; do
   for lib in anothertls_amd/variants/libatls_*.so; do
     n=$(basename $lib .so)
-    for cfg in c2_aes128gcm_64Ki_x_16KiB c4_aes256gcm_1Mi_x_16KiB; do
+    for cfg in ${CONFIGS:-c2_aes128gcm_64Ki_x_16KiB c4_aes256gcm_1Mi_x_16KiB}; do
       r=$(ATLS_LIB=$PWD/$lib timeout -k 10 120 python bench.py --config $cfg --no-cpu-baseline 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['kernel_ms'])") || exit 1
       echo "round $round $n $cfg: $r"
     done
