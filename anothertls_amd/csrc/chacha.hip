@@ -108,7 +108,11 @@ __device__ __forceinline__ void chacha_block(const uint32_t kw[8], uint32_t ctr,
   uint32_t x0 = 0x61707865, x1 = 0x3320646e, x2 = 0x79622d32, x3 = 0x6b206574;
   uint32_t x4 = kw[0], x5 = kw[1], x6 = kw[2], x7 = kw[3], x8 = kw[4], x9 = kw[5], x10 = kw[6], x11 = kw[7];
   uint32_t x12 = ctr, x13 = nw[0], x14 = nw[1], x15 = nw[2];
-#pragma unroll 2
+#ifndef ATLS_CHACHA_UNROLL
+#define ATLS_CHACHA_UNROLL 2  // double rounds per loop trip: 1 / 5 / 10 measured no better (C5 +1 / +2 / +5 %,
+                              // profiles/r02/ab_chacha_unroll.log)
+#endif
+#pragma unroll ATLS_CHACHA_UNROLL
   for (int i = 0; i < 10; i++) {
     QR(x0, x4, x8, x12) QR(x1, x5, x9, x13) QR(x2, x6, x10, x14) QR(x3, x7, x11, x15)
     QR(x0, x5, x10, x15) QR(x1, x6, x11, x12) QR(x2, x7, x8, x13) QR(x3, x4, x9, x14)
