@@ -509,6 +509,18 @@ __global__ __launch_bounds__(256, PLANNED ? ATLS_CHACHA_MINW_SIDE : OPEN ? ATLS_
   else chacha_direct<OPEN>(A, lane);
 }
 
+// Latency path for a few records (the Cipher-trait single call, record.rs:191-193): one record per
+// wave at 64 lanes, so a 1.5 KiB record's 26 ChaCha blocks run side by side instead of 13 deep at
+// 2 lanes (the per-record Poly1305 scan is 6 levels instead of 1; throughput is not the point).
+#ifndef ATLS_CHACHA_LAT_MAX
+#define ATLS_CHACHA_LAT_MAX 32  // direct batches of at most this many records
+#endif
+template <bool OPEN>
+__global__ __launch_bounds__(64) void chacha_kernel_lat(ChArgs A) {
+  const WorkList W{nullptr, nullptr, kListChacha, A.n};
+  chacha_group<OPEN, 64>(A, W, blockIdx.x, A.n, (int)(threadIdx.x & 63));
+}
+
 }  // namespace atls
 
 // idx / plan: the batch plan's work lists (G = 16), or nullptr for a direct batch (per-step widths).
@@ -523,7 +535,10 @@ extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs
   // strides over 16 positions per wave and simply finishes its list sooner
   const uint32_t want16 = (n + 15u) / 16u;
   const uint32_t g = (uint32_t)grid < want16 ? (uint32_t)grid : want16;
-  if (idx) {
+  if (!idx && n <= (uint32_t)ATLS_CHACHA_LAT_MAX) {
+    if (open) hipLaunchKernelGGL((atls::chacha_kernel_lat<true>), dim3(n), dim3(64), 0, s, A);
+    else hipLaunchKernelGGL((atls::chacha_kernel_lat<false>), dim3(n), dim3(64), 0, s, A);
+  } else if (idx) {
     if (open) hipLaunchKernelGGL((atls::chacha_kernel<true, true>), dim3(g), dim3(256), 0, s, A);
     else hipLaunchKernelGGL((atls::chacha_kernel<false, true>), dim3(g), dim3(256), 0, s, A);
   } else {

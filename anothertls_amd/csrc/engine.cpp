@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -21,6 +22,7 @@
 
 #include "../../include/atls.h"
 #include "atls_dev.h"
+#include "engine_internal.h"
 #include "plan.h"
 
 extern "C" int atls_launch_build_t0(uint32_t* t0, hipStream_t s);
@@ -414,12 +416,13 @@ int install_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t 
 
 // ---- Cipher-trait calls (atls_seal / atls_open / atls_aes_block) ------------------------------
 // The reference's record layer calls Cipher::encrypt / decrypt once per record from any thread
-// (Arc<dyn Cipher + Send + Sync>, ciphersuite.rs:78-87, record.rs:191-193). Each calling thread
-// gets its own engines (one per kind of key: AES-128 / -192 / -256 / ChaCha20, so every call is a
-// direct single-kernel batch) with a small key cache, pinned staging and its own streams: calls of
-// different threads run concurrently, and a repeated key costs no key setup (the reference
-// re-expands the key and recomputes H on every call, gcm.rs:52-56). Contexts of finished threads
-// go back to a pool for the next thread.
+// (Arc<dyn Cipher + Send + Sync>, ciphersuite.rs:78-87, record.rs:191-193). A call leases a context
+// from a bounded pool (at most ATLS_SINGLE_CONTEXTS, default 8; further callers wait for one): its
+// own engines (one per kind of key: AES-128 / -192 / -256 / ChaCha20, so every call is a direct
+// single-kernel batch) with a small key cache, pinned staging and its own streams. Calls of
+// different threads run concurrently, a thread gets back the context it used last when it is free
+// (its key cache), and a repeated key costs no key setup (the reference re-expands the key and
+// recomputes H on every call, gcm.rs:52-56).
 constexpr uint32_t kCacheSlots = 16;
 
 struct KindEngine {
@@ -430,58 +433,90 @@ struct KindEngine {
 
 struct SingleCtx {
   KindEngine kinds[4];  // AES-128, AES-192, AES-256, ChaCha20-Poly1305
-  uint8_t* pin = nullptr;
+  uint8_t* pin = nullptr;  // page-locked, mapped into the device's address space
+  uint8_t* pin_dev = nullptr;
   size_t pin_cap = 0;
   bool reserve_pin(size_t n) {
     if (n <= pin_cap) return true;
     if (pin) (void)hipHostFree(pin);
-    pin = nullptr;
+    pin = pin_dev = nullptr;
     pin_cap = 0;
     size_t c = std::max<size_t>(n, size_t(1) << 16);
     void* p = nullptr;
-    if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) return false;
+    void* pd = nullptr;
+    // fine-grained (coherent): the kernel's reads of the block see the host's latest writes and its
+    // writes reach the host without a cache write-back
+    if (hipHostMalloc(&p, c, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return false;
+    if (hipHostGetDevicePointer(&pd, p, 0) != hipSuccess) {
+      (void)hipHostFree(p);
+      return false;
+    }
     pin = (uint8_t*)p;
+    pin_dev = (uint8_t*)pd;
     pin_cap = c;
     return true;
   }
 };
 
-std::mutex g_pool_mu;
-std::vector<SingleCtx*>& ctx_pool() {
-  static std::vector<SingleCtx*>* pool = new std::vector<SingleCtx*>();  // never destroyed: outlives threads
+struct CtxPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<SingleCtx*> free;
+  size_t created = 0;
+  size_t max = [] {
+    const char* v = std::getenv("ATLS_SINGLE_CONTEXTS");
+    const long n = v ? std::atol(v) : 8;
+    return (size_t)(n > 0 ? n : 8);
+  }();
+};
+CtxPool& ctx_pool() {
+  static CtxPool* pool = new CtxPool();  // never destroyed: outlives every thread
   return *pool;
 }
 
+// A context for the duration of one call; back to the pool when the lease ends.
 struct CtxLease {
   SingleCtx* c = nullptr;
-  ~CtxLease() {
-    if (c) {
-      std::lock_guard<std::mutex> lk(g_pool_mu);
-      ctx_pool().push_back(c);
+  CtxLease() {
+    thread_local SingleCtx* last = nullptr;
+    CtxPool& P = ctx_pool();
+    std::unique_lock<std::mutex> lk(P.mu);
+    for (;;) {
+      auto it = std::find(P.free.begin(), P.free.end(), last);
+      if (last && it != P.free.end()) {
+        c = last;
+        P.free.erase(it);
+      } else if (!P.free.empty()) {
+        c = P.free.back();
+        P.free.pop_back();
+      } else if (P.created < P.max) {
+        c = new (std::nothrow) SingleCtx();
+        if (c) P.created++;
+      } else {
+        P.cv.wait(lk);
+        continue;
+      }
+      break;
     }
+    last = c;
+  }
+  ~CtxLease() {
+    if (!c) return;
+    CtxPool& P = ctx_pool();
+    {
+      std::lock_guard<std::mutex> lk(P.mu);
+      P.free.push_back(c);
+    }
+    P.cv.notify_one();
   }
 };
-
-SingleCtx* this_thread_ctx() {
-  thread_local CtxLease lease;
-  if (!lease.c) {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    if (!ctx_pool().empty()) {
-      lease.c = ctx_pool().back();
-      ctx_pool().pop_back();
-    } else {
-      lease.c = new (std::nothrow) SingleCtx();
-    }
-  }
-  return lease.c;
-}
 
 int kind_of(uint16_t suite, size_t key_len) {
   if (suite == ATLS_TLS_CHACHA20_POLY1305_SHA256) return 3;
   return key_len == 16 ? 0 : key_len == 24 ? 1 : 2;
 }
 
-// Slot of this key in the thread's engine of its kind, installing it (LRU eviction) on a miss.
+// Slot of this key in the context's engine of its kind, installing it (LRU eviction) on a miss.
 int cached_slot(SingleCtx* c, uint16_t suite, const uint8_t* key, size_t key_len, atls_engine** eng, uint32_t* slot) {
   KindEngine& k = c->kinds[kind_of(suite, key_len)];
   if (!k.e) {
@@ -519,9 +554,28 @@ int cached_slot(SingleCtx* c, uint16_t suite, const uint8_t* key, size_t key_len
   return ATLS_OK;
 }
 
-// One Cipher::encrypt / decrypt call as a single RAW record on this thread's engine: the input,
-// nonce and AAD go through pinned staging into the engine's device buffers, one direct launch,
-// and the result comes back in one synchronisation.
+// Records up to this many bytes are read by the kernel straight from the pinned staging block
+// (mapped host memory, no copy); longer ones are staged to the device in one copy (the kernel's
+// per-step loads over PCIe would cost more than the copy). Outputs always go straight to the
+// pinned block. ATLS_SINGLE_ZC_MAX overrides (tuning).
+size_t single_zero_copy_max() {
+  static const size_t v = [] {
+    const char* e = std::getenv("ATLS_SINGLE_ZC_MAX");
+    return e ? (size_t)std::atol(e) : (size_t)4096;
+  }();
+  return v;
+}
+
+// 128-bit canary in the pinned tag slot of a seal: a kernel that refused the record leaves it in
+// place. Refusals cannot happen here (the descriptor is built and checked on the host exactly as
+// direct_reject checks it); the canary keeps a refusal from passing unnoticed all the same, at a
+// false-alarm rate of 2^-128.
+constexpr uint32_t kTagCanary[4] = {0x6c1f9a3du, 0xb2e4570cu, 0x93d0e8a1u, 0x0f7b2c56u};
+
+// One Cipher::encrypt / decrypt call as a single RAW record: descriptor, tag, IV, AAD and input
+// are written into the context's pinned block, the kernel reads them there (or from one copy of
+// the block for long records) and writes output, tag and result straight back into it, and one
+// stream synchronisation ends the call. No other copy and no descriptor upload.
 int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
            const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, const uint8_t* tag_in, size_t tag_len,
            uint8_t* out, uint8_t* tag_out) {
@@ -538,52 +592,56 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
   }
   if (iv_len > 255 || aad_len > 0xffff || len > 0xffffffffull) return ATLS_ILLEGAL_PARAMETER;
   if (open && tag_len != 16) return ATLS_BAD_RECORD_MAC;  // `T != auth_tag` with a wrong-length slice
-  SingleCtx* c = this_thread_ctx();
+  CtxLease lease;
+  SingleCtx* c = lease.c;
   if (!c) return ATLS_INTERNAL_ERROR;
   atls_engine* e = nullptr;
   uint32_t slot = 0;
   int rc = cached_slot(c, suite, key, key_len, &e, &slot);
   if (rc) return rc;
-  const size_t aux_len = iv_len + aad_len;
-  const size_t in_at = 0, aux_at = (len + 15) & ~size_t(15), tag_at = (aux_at + aux_len + 15) & ~size_t(15);
-  const size_t res_at = tag_at + 16, err_at = res_at + 8, total = err_at + 8;
+  // pinned block: descriptor | tag | open result | iv || aad | input | output
+  const size_t rec_at = 0, tag_at = 64, res_at = 80, aux_at = 96;
+  const size_t in_at = (aux_at + iv_len + aad_len + 15) & ~size_t(15);
+  const size_t out_at = (in_at + len + 15) & ~size_t(15), total = out_at + len + 16;
   if (!c->reserve_pin(total)) return ATLS_INTERNAL_ERROR;
   uint8_t* h = c->pin;
-  if (len) std::memcpy(h + in_at, in, len);
-  if (iv_len) std::memcpy(h + aux_at, iv, iv_len);
-  if (aad_len) std::memcpy(h + aux_at + iv_len, aad, aad_len);
-  if (open) std::memcpy(h + tag_at, tag_in, 16);
   atls_rec r;
   std::memset(&r, 0, sizeof r);
+  r.in_off = in_at;
+  r.out_off = out_at;
+  r.aux_off = aux_at;
   r.len = (uint32_t)len;
   r.key_slot = slot;
   r.mode = ATLS_MODE_RAW;
   r.iv_len = (uint8_t)iv_len;
   r.aad_len = (uint16_t)aad_len;
+  std::memcpy(h + rec_at, &r, sizeof r);
+  if (open) {
+    std::memcpy(h + tag_at, tag_in, 16);
+    std::memset(h + res_at, 0xff, sizeof(atls_open_result));  // the kernel writes every field
+  } else {
+    std::memcpy(h + tag_at, kTagCanary, 16);
+  }
+  if (iv_len) std::memcpy(h + aux_at, iv, iv_len);
+  if (aad_len) std::memcpy(h + aux_at + iv_len, aad, aad_len);
+  if (len) std::memcpy(h + in_at, in, len);
   std::lock_guard<std::mutex> lk(e->mu);
-  if (!set_dev(e) || !e->in.reserve(total + 16) || !e->out.reserve(len + 16)) return ATLS_INTERNAL_ERROR;
-  uint8_t* d = (uint8_t*)e->in.p;
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
   hipStream_t s = e->stream;
-  if (hipMemcpyAsync(d, h, res_at, hipMemcpyHostToDevice, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
-  // a RAW record's descriptor offsets are relative to the staged block above
-  r.in_off = in_at;
-  r.aux_off = 0;
-  if (!e->recs.reserve(sizeof(atls_rec)) ||
-      hipMemcpyAsync(e->recs.p, &r, sizeof r, hipMemcpyHostToDevice, s) != hipSuccess)
-    return ATLS_INTERNAL_ERROR;
-  uint8_t* dout = (uint8_t*)e->out.p;
-  atls_open_result* dres = (atls_open_result*)(d + res_at);
-  rc = launch_records(e, open, (const atls_rec*)e->recs.p, 1, d, d + aux_at, dout, d + tag_at, d + tag_at, dres, s, 0);
+  uint8_t* hd = c->pin_dev;
+  const uint8_t* src = hd;  // descriptor, aux, tag-in and input: read in place ...
+  if (len > single_zero_copy_max()) {  // ... or from one copy of the block
+    if (!e->in.reserve(out_at) || hipMemcpyAsync(e->in.p, h, out_at, hipMemcpyHostToDevice, s) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    src = (const uint8_t*)e->in.p;
+  }
+  rc = launch_records(e, open, (const atls_rec*)(src + rec_at), 1, src, src, hd, hd + tag_at, src + tag_at,
+                      (atls_open_result*)(hd + res_at), s, 0);
   if (rc) return rc;
-  if (len && hipMemcpyAsync(h + in_at, dout, len, hipMemcpyDeviceToHost, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
-  if (hipMemcpyAsync(h + tag_at, d + tag_at, 16 + sizeof(atls_open_result), hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipMemcpyAsync(h + err_at, e->err.p, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
-    return ATLS_INTERNAL_ERROR;
-  uint32_t err = 0;
-  std::memcpy(&err, h + err_at, 4);
-  if ((rc = take_err(e, err))) return rc;
+  if (hipStreamSynchronize(s) != hipSuccess) return ATLS_INTERNAL_ERROR;
   if (!open) {
-    if (len) std::memcpy(out, h + in_at, len);
+    if (std::memcmp(h + tag_at, kTagCanary, 16) == 0) return ATLS_ILLEGAL_PARAMETER;
+    if (len) std::memcpy(out, h + out_at, len);
     std::memcpy(tag_out, h + tag_at, 16);
     return ATLS_OK;
   }
@@ -593,11 +651,17 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
     if (len) std::memset(out, 0, len);  // no unauthenticated plaintext leaves (reference returns Err)
     return res.status;
   }
-  if (len) std::memcpy(out, h + in_at, len);
+  if (len) std::memcpy(out, h + out_at, len);
   return ATLS_OK;
 }
 
 }  // namespace
+
+uint32_t atls::engine_slots(atls_engine* e) {
+  if (!e) return 0;
+  std::lock_guard<std::mutex> lk(e->mu);
+  return e->n_slots;
+}
 
 extern "C" {
 
@@ -726,8 +790,9 @@ int atls_hash_batch(atls_engine* e, int op, uint32_t hash_len, const uint8_t* da
   if (op == ATLS_HASH_HKDF_EXPAND ? out_len > 255u * hash_len : out_len != hash_len)
     return ATLS_ILLEGAL_PARAMETER;  // hkdf.rs:38 returns None past 255 * HashLen
   for (uint32_t i = 0; i < n; i++) {  // every span inside data
-    if (msgs[i].off + msgs[i].len > data_len) return ATLS_ILLEGAL_PARAMETER;
-    if (op != ATLS_HASH_SHA && keys[i].off + keys[i].len > data_len) return ATLS_ILLEGAL_PARAMETER;
+    if (msgs[i].off > data_len || msgs[i].len > data_len - msgs[i].off) return ATLS_ILLEGAL_PARAMETER;
+    if (op != ATLS_HASH_SHA && (keys[i].off > data_len || keys[i].len > data_len - keys[i].off))
+      return ATLS_ILLEGAL_PARAMETER;
   }
   if (n == 0) return ATLS_OK;
   std::lock_guard<std::mutex> lk(e->mu);
@@ -802,7 +867,8 @@ int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* 
 
 int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_t in[16], uint8_t out[16]) {
   if (key_len != 16 && key_len != 24 && key_len != 32) return ATLS_ILLEGAL_PARAMETER;  // AES::init key sizes
-  SingleCtx* c = this_thread_ctx();
+  CtxLease lease;
+  SingleCtx* c = lease.c;
   if (!c) return ATLS_INTERNAL_ERROR;
   atls_engine* e = nullptr;
   uint32_t slot = 0;

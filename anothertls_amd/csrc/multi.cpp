@@ -16,33 +16,58 @@
 // device list with repeats (several ranges on one GPU: tests on a one-GPU box) uses HIP
 // device-to-device copies instead. Host-memory batches need no exchange: each device stages its
 // own range over its own PCIe link, one host thread per device.
+//
+// Descriptors are validated before anything is queued, and a failure after that point waits for
+// the queued transfers and kernels (drain) before returning, so the caller's buffers are never
+// touched after the call returns. ATLS_MULTI_RCCL_SELF=1 with one device repeated runs the RCCL
+// branch as rank-0-to-itself send / recv on a one-rank communicator (the one-GPU test of the
+// RCCL binding, tests/test_gpu_dist.py).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
+#include <rccl/rccl.h>
+
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/atls.h"
+#include "engine_internal.h"
 
 namespace {
 
 // ---- the few RCCL entry points we use, resolved at run time ------------------------------
-typedef struct ncclComm* ncclComm_t;
-typedef int ncclResult_t;  // ncclSuccess = 0
-constexpr int kNcclUint8 = 1;
+// rccl.h gives the types and the prototypes; the library itself is dlopen'ed (the librccl.so.1
+// PyTorch may already hold), and every resolved pointer has exactly the header's type.
 struct Rccl {
-  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
-  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
-  ncclResult_t (*group_start)() = nullptr;
-  ncclResult_t (*group_end)() = nullptr;
-  ncclResult_t (*send)(const void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
-  ncclResult_t (*recv)(void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
+  decltype(&ncclCommInitAll) comm_init_all = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclSend) send = nullptr;
+  decltype(&ncclRecv) recv = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
   bool ok = false;
 };
+static_assert(std::is_same<decltype(Rccl::send), ncclResult_t (*)(const void*, size_t, ncclDataType_t, int, ncclComm_t,
+                                                                  hipStream_t)>::value,
+              "ncclSend prototype");
+static_assert(std::is_same<decltype(Rccl::recv), ncclResult_t (*)(void*, size_t, ncclDataType_t, int, ncclComm_t,
+                                                                  hipStream_t)>::value,
+              "ncclRecv prototype");
+static_assert(std::is_same<decltype(Rccl::comm_init_all), ncclResult_t (*)(ncclComm_t*, int, const int*)>::value,
+              "ncclCommInitAll prototype");
+static_assert(ncclSuccess == 0 && ncclUint8 == 1, "rccl.h enums");
+
+template <typename F>
+void resolve(void* h, const char* name, F& f) {
+  f = reinterpret_cast<F>(dlsym(h, name));
+}
 
 const Rccl& rccl() {
   static Rccl r;
@@ -51,12 +76,13 @@ const Rccl& rccl() {
     void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
     if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
     if (!h) return;
-    r.comm_init_all = (ncclResult_t(*)(ncclComm_t*, int, const int*))dlsym(h, "ncclCommInitAll");
-    r.comm_destroy = (ncclResult_t(*)(ncclComm_t))dlsym(h, "ncclCommDestroy");
-    r.group_start = (ncclResult_t(*)())dlsym(h, "ncclGroupStart");
-    r.group_end = (ncclResult_t(*)())dlsym(h, "ncclGroupEnd");
-    r.send = (ncclResult_t(*)(const void*, size_t, int, int, ncclComm_t, hipStream_t))dlsym(h, "ncclSend");
-    r.recv = (ncclResult_t(*)(void*, size_t, int, int, ncclComm_t, hipStream_t))dlsym(h, "ncclRecv");
+    resolve(h, "ncclCommInitAll", r.comm_init_all);
+    resolve(h, "ncclCommDestroy", r.comm_destroy);
+    resolve(h, "ncclGroupStart", r.group_start);
+    resolve(h, "ncclGroupEnd", r.group_end);
+    resolve(h, "ncclSend", r.send);
+    resolve(h, "ncclRecv", r.recv);
+    resolve(h, "ncclGetErrorString", r.error_string);
     r.ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.send && r.recv;
   });
   return r;
@@ -102,12 +128,27 @@ size_t out_len(const atls_rec& r, bool open) {
 
 struct atls_multi {
   std::vector<Part> parts;
-  std::vector<ncclComm_t> comms;  // one per device when all devices are distinct
+  std::vector<ncclComm_t> comms;  // one per device when all devices are distinct (one in self mode)
   bool use_rccl = false;
+  // ATLS_MULTI_RCCL_SELF=1 with one device repeated: a one-rank communicator, and every part's
+  // transfers are RCCL send / recv of rank 0 to itself on the root's transfer stream. The batch
+  // then goes through exactly the RCCL branch of run_device on a one-GPU box (tests).
+  bool rccl_self = false;
   std::mutex mu;
 };
 
 namespace {
+
+// Wait for everything queued for this batch (engine streams, transfer streams), and clear the
+// part engines' sticky error words, so an early return never leaves work that reads or writes
+// the caller's buffers, and no refusal of this batch is reported by a later call.
+void drain(atls_multi* m) {
+  for (Part& q : m->parts) {
+    (void)atls_engine_sync(q.eng);
+    (void)hipSetDevice(q.device);
+    (void)hipStreamSynchronize(q.comm);
+  }
+}
 
 // Device-resident batch on the root device. first[p] .. first[p+1] = records of part p.
 int run_device(atls_multi* m, bool open, const atls_rec* recs, const uint32_t* first, const uint8_t* in,
@@ -131,6 +172,11 @@ int run_device(atls_multi* m, bool open, const atls_rec* recs, const uint32_t* f
     r.in_hi = recs[r.b - 1].in_off + in_len(recs[r.b - 1], open);
     r.out_hi = recs[r.b - 1].out_off + out_len(recs[r.b - 1], open);
   }
+  // Where part p's side of a transfer runs: its own device, comm rank and stream over RCCL between
+  // distinct devices; the root's otherwise (device copies, or RCCL self mode).
+  const bool own_side = m->use_rccl && !m->rccl_self;
+  auto side_stream = [&](size_t p) { return own_side ? m->parts[p].comm : root.comm; };
+  auto side_device = [&](size_t p) { return own_side ? m->parts[p].device : root.device; };
   // Root work is ordered after the caller's prior work on the root device (its engine stream).
   if (hipSetDevice(root.device) != hipSuccess || hipEventRecord(root.ev_in, (hipStream_t)atls_engine_stream(root.eng)) != hipSuccess ||
       hipStreamWaitEvent(root.comm, root.ev_in, 0) != hipSuccess)
@@ -148,47 +194,54 @@ int run_device(atls_multi* m, bool open, const atls_rec* recs, const uint32_t* f
     }
     if (!q.in.reserve(r.in_hi - r.in_lo + 16) || !q.out.reserve(r.out_hi - r.out_lo + 16) || !q.aux.reserve(aux_end + 16) ||
         !q.tags.reserve(16 * (size_t)cnt) || !q.res.reserve(sizeof(atls_open_result) * (size_t)cnt))
-      return ATLS_INTERNAL_ERROR;
+      return ATLS_INTERNAL_ERROR;  // nothing queued yet but the root's event wait
   }
-  // ---- scatter: input ranges, aux, (open) tags ----
+  // ---- scatter: input ranges, aux, (open) tags; gather: output ranges, tags, results ----
   auto xfer = [&](bool to_parts) -> int {
     if (m->use_rccl) {
       const Rccl& R = rccl();
-      if (R.group_start()) return ATLS_INTERNAL_ERROR;
+      if (R.group_start() != ncclSuccess) return ATLS_INTERNAL_ERROR;
+      ncclResult_t bad = ncclSuccess;
+      auto chk = [&](ncclResult_t r) {
+        if (r != ncclSuccess && bad == ncclSuccess) bad = r;
+      };
       for (size_t p = 1; p < P; p++) {
         Part& q = m->parts[p];
         const Range& r = rg[p];
         const uint32_t cnt = r.b - r.a;
         if (!cnt) continue;
-        const int pp = (int)p;
-        ncclComm_t rc = m->comms[0], qc = m->comms[p];
+        // root = rank 0; part p = rank p, or rank 0 itself in self mode
+        const int peer = m->rccl_self ? 0 : (int)p;
+        ncclComm_t rc = m->comms[0], qc = m->comms[m->rccl_self ? 0 : p];
+        hipStream_t qs = side_stream(p);
         if (to_parts) {
-          R.send(in + r.in_lo, r.in_hi - r.in_lo, kNcclUint8, pp, rc, root.comm);
-          R.recv(q.in.p, r.in_hi - r.in_lo, kNcclUint8, 0, qc, q.comm);
-          R.send(out + r.out_lo, r.out_hi - r.out_lo, kNcclUint8, pp, rc, root.comm);  // bytes between records
-          R.recv(q.out.p, r.out_hi - r.out_lo, kNcclUint8, 0, qc, q.comm);
+          chk(R.send(in + r.in_lo, r.in_hi - r.in_lo, ncclUint8, peer, rc, root.comm));
+          chk(R.recv(q.in.p, r.in_hi - r.in_lo, ncclUint8, 0, qc, qs));
+          chk(R.send(out + r.out_lo, r.out_hi - r.out_lo, ncclUint8, peer, rc, root.comm));  // bytes between records
+          chk(R.recv(q.out.p, r.out_hi - r.out_lo, ncclUint8, 0, qc, qs));
           if (aux_end) {
-            R.send(aux, aux_end, kNcclUint8, pp, rc, root.comm);
-            R.recv(q.aux.p, aux_end, kNcclUint8, 0, qc, q.comm);
+            chk(R.send(aux, aux_end, ncclUint8, peer, rc, root.comm));
+            chk(R.recv(q.aux.p, aux_end, ncclUint8, 0, qc, qs));
           }
           if (open && tags_in) {
-            R.send(tags_in + 16 * (size_t)r.a, 16 * (size_t)cnt, kNcclUint8, pp, rc, root.comm);
-            R.recv(q.tags.p, 16 * (size_t)cnt, kNcclUint8, 0, qc, q.comm);
+            chk(R.send(tags_in + 16 * (size_t)r.a, 16 * (size_t)cnt, ncclUint8, peer, rc, root.comm));
+            chk(R.recv(q.tags.p, 16 * (size_t)cnt, ncclUint8, 0, qc, qs));
           }
         } else {
-          R.send(q.out.p, r.out_hi - r.out_lo, kNcclUint8, 0, qc, q.comm);
-          R.recv(out + r.out_lo, r.out_hi - r.out_lo, kNcclUint8, pp, rc, root.comm);
+          chk(R.send(q.out.p, r.out_hi - r.out_lo, ncclUint8, 0, qc, qs));
+          chk(R.recv(out + r.out_lo, r.out_hi - r.out_lo, ncclUint8, peer, rc, root.comm));
           if (!open && tags_out) {
-            R.send(q.tags.p, 16 * (size_t)cnt, kNcclUint8, 0, qc, q.comm);
-            R.recv(tags_out + 16 * (size_t)r.a, 16 * (size_t)cnt, kNcclUint8, pp, rc, root.comm);
+            chk(R.send(q.tags.p, 16 * (size_t)cnt, ncclUint8, 0, qc, qs));
+            chk(R.recv(tags_out + 16 * (size_t)r.a, 16 * (size_t)cnt, ncclUint8, peer, rc, root.comm));
           }
           if (open) {
-            R.send(q.res.p, sizeof(atls_open_result) * (size_t)cnt, kNcclUint8, 0, qc, q.comm);
-            R.recv(res + r.a, sizeof(atls_open_result) * (size_t)cnt, kNcclUint8, pp, rc, root.comm);
+            chk(R.send(q.res.p, sizeof(atls_open_result) * (size_t)cnt, ncclUint8, 0, qc, qs));
+            chk(R.recv(res + r.a, sizeof(atls_open_result) * (size_t)cnt, ncclUint8, peer, rc, root.comm));
           }
         }
       }
-      return R.group_end() ? ATLS_INTERNAL_ERROR : ATLS_OK;
+      chk(R.group_end());  // always closes the group, also after a failed call inside it
+      return bad == ncclSuccess ? ATLS_OK : ATLS_INTERNAL_ERROR;
     }
     // device-to-device copies (repeated devices): issued on the root's transfer stream
     if (hipSetDevice(root.device) != hipSuccess) return ATLS_INTERNAL_ERROR;
@@ -216,16 +269,20 @@ int run_device(atls_multi* m, bool open, const atls_rec* recs, const uint32_t* f
     }
     return ATLS_OK;
   };
+  // From here on work is queued: every failure drains it before returning.
+  auto fail = [&](int rc) {
+    drain(m);
+    return rc;
+  };
   int rc = xfer(true);
-  if (rc) return rc;
+  if (rc) return fail(rc);
   // inputs in place -> every part's engine stream may start
   for (size_t p = 1; p < P; p++) {
     Part& q = m->parts[p];
     if (rg[p].a == rg[p].b) continue;
-    hipStream_t src = m->use_rccl ? q.comm : root.comm;
-    if (hipSetDevice(m->use_rccl ? q.device : root.device) != hipSuccess || hipEventRecord(q.ev_in, src) != hipSuccess ||
+    if (hipSetDevice(side_device(p)) != hipSuccess || hipEventRecord(q.ev_in, side_stream(p)) != hipSuccess ||
         hipSetDevice(q.device) != hipSuccess || hipStreamWaitEvent((hipStream_t)atls_engine_stream(q.eng), q.ev_in, 0) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
   }
   // ---- every part seals / opens its range (the root in place, beside the transfers) ----
   for (size_t p = 0; p < P; p++) {
@@ -245,21 +302,20 @@ int run_device(atls_multi* m, bool open, const atls_rec* recs, const uint32_t* f
                 : atls_seal_batch(q.eng, q.recs.data(), cnt, q.in.p, q.aux.p, q.out.p,
                                   want_tags ? (uint8_t*)q.tags.p : nullptr, dflags);
     }
-    if (rc) return rc;
+    if (rc) return fail(rc);
     if (p && (hipSetDevice(q.device) != hipSuccess || hipEventRecord(q.ev_done, (hipStream_t)atls_engine_stream(q.eng)) != hipSuccess))
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
   }
   // ---- gather ----
   for (size_t p = 1; p < P; p++) {
     Part& q = m->parts[p];
     if (rg[p].a == rg[p].b) continue;
-    hipStream_t dst = m->use_rccl ? q.comm : root.comm;
-    if (hipSetDevice(m->use_rccl ? q.device : root.device) != hipSuccess || hipStreamWaitEvent(dst, q.ev_done, 0) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+    if (hipSetDevice(side_device(p)) != hipSuccess || hipStreamWaitEvent(side_stream(p), q.ev_done, 0) != hipSuccess)
+      return fail(ATLS_INTERNAL_ERROR);
   }
   rc = xfer(false);
-  if (rc) return rc;
-  // every part's status (sticky error words), then the root's transfer stream
+  if (rc) return fail(rc);
+  // every part's status (sticky error words), then the transfer streams
   int status = ATLS_OK;
   for (size_t p = 0; p < P; p++) {
     if (rg[p].a == rg[p].b) continue;
@@ -268,7 +324,7 @@ int run_device(atls_multi* m, bool open, const atls_rec* recs, const uint32_t* f
   }
   for (size_t p = 0; p < P; p++) {
     if (hipSetDevice(m->parts[p].device) != hipSuccess || hipStreamSynchronize(m->parts[p].comm) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
   }
   return status;
 }
@@ -315,6 +371,12 @@ int run(atls_multi* m, bool open, const atls_rec* recs, uint32_t n, const void* 
       return ATLS_ILLEGAL_PARAMETER;
     if (recs[i].mode == ATLS_MODE_RAW) aux_end = std::max(aux_end, (size_t)recs[i].aux_off + recs[i].iv_len + recs[i].aad_len);
   }
+  // refused descriptors are refused before anything is queued (as run_batch does for one engine)
+  const uint32_t n_slots = atls::engine_slots(m->parts[0].eng);  // every part holds the same key table
+  const bool no_tags = open ? !tags_in : !tags_out;
+  for (uint32_t i = 0; i < n; i++)
+    if (recs[i].key_slot >= n_slots || recs[i].mode > ATLS_MODE_WIRE || (no_tags && recs[i].mode != ATLS_MODE_WIRE))
+      return ATLS_ILLEGAL_PARAMETER;
   std::lock_guard<std::mutex> lk(m->mu);
   const uint32_t P = (uint32_t)m->parts.size();
   std::vector<uint32_t> first(P + 1);
@@ -371,15 +433,20 @@ atls_multi* atls_multi_create(const int* devices, int n_devices) {
       return nullptr;
     }
   }
-  if (distinct && n_devices > 1) {
+  const char* self_env = std::getenv("ATLS_MULTI_RCCL_SELF");
+  const bool self = !distinct && self_env && std::atoi(self_env) != 0 &&
+                    std::all_of(devices, devices + n_devices, [&](int d) { return d == devices[0]; });
+  if ((distinct || self) && n_devices > 1) {
     const Rccl& R = rccl();
-    m->comms.assign((size_t)n_devices, nullptr);
-    if (!R.ok || R.comm_init_all(m->comms.data(), n_devices, devices) != 0) {
+    const int ranks = self ? 1 : n_devices;
+    m->comms.assign((size_t)ranks, nullptr);
+    if (!R.ok || R.comm_init_all(m->comms.data(), ranks, devices) != ncclSuccess) {
       m->comms.clear();
       atls_multi_destroy(m);
       return nullptr;
     }
     m->use_rccl = true;
+    m->rccl_self = self;
   }
   return m;
 }

@@ -33,6 +33,56 @@ def init(backend, device=None):
     return True
 
 
+def world_size():
+    """World size of the joined process group (1 when there is none)."""
+    return tdist.get_world_size() if (tdist.is_available() and tdist.is_initialized()) else 1
+
+
+def launch_ranks(argv, n, timeout_s=None):
+    """Start n copies of `argv` (a Python script and its arguments) as rank processes on this
+    node -- RANK = LOCAL_RANK = 0..n-1, WORLD_SIZE = n, MASTER_ADDR 127.0.0.1 and a free port, as
+    torch.distributed.run sets them -- and wait for them. The caller must not have touched the GPU
+    (each rank is a fresh process that opens its own device). When a rank fails, the others are
+    ended (by their own PIDs). Returns the first non-zero exit status, else 0."""
+    import signal
+    import socket
+    import subprocess
+    import sys
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, *argv], env=env))
+    status, t0 = 0, time.monotonic()
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+        if status or (timeout_s is not None and time.monotonic() - t0 > timeout_s):
+            for p in live:  # a failed or overdue rank: end the others, then collect them
+                p.send_signal(signal.SIGTERM)
+            for p in live:
+                try:
+                    p.wait(30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            if not status:
+                status = WATCHDOG_EXIT
+            break
+        time.sleep(0.05)
+    return status
+
+
 def barrier():
     if tdist.is_available() and tdist.is_initialized():
         tdist.barrier()
@@ -141,11 +191,15 @@ def seal_sharded(seal, recs, inp=None, out=None, tags=None, device=None):
     return a, b
 
 
+WATCHDOG_EXIT = 3  # status of a process whose watchdog fired (a hung step is a failure, not success)
+
+
 def run_or_exit(fn, timeout_s, on_timeout):
     """fn() with a watchdog: if it has not returned after timeout_s seconds, on_timeout() runs
-    (e.g. print the result gathered so far) and the process exits with status 0 -- for steps
-    after a benchmark's timed region whose collectives could hang (a hung rank must not cost the
-    measured line). Returns (True, fn's value) or (False, the exception fn raised)."""
+    (e.g. print the result gathered so far) and the process exits with status WATCHDOG_EXIT -- for
+    steps after a benchmark's timed region whose collectives could hang (the measured line is
+    still printed, and the non-zero status says something hung). Returns (True, fn's value) or
+    (False, the exception fn raised)."""
     import threading
 
     lock, state = threading.Lock(), {"done": False}
@@ -158,7 +212,7 @@ def run_or_exit(fn, timeout_s, on_timeout):
             try:
                 on_timeout()
             finally:
-                os._exit(0)
+                os._exit(WATCHDOG_EXIT)
 
     timer = threading.Timer(timeout_s, fire)
     timer.daemon = True

@@ -6,7 +6,11 @@ path, MB/s, with the reference's per-record CPU path as cpu_baseline)
 For N > 1 the driver launches one rank per GPU with torch.distributed.run; each rank seals
 its own pre-sharded, device-resident batch of the config (records are independent, so there
 is no data-path collective: weak scaling). One step = one atls_seal_batch over the whole
-batch. Rank 0 prints one JSON line.
+batch. Rank 0 prints one JSON line. `--gpus N` without a launcher (no WORLD_SIZE) starts the N
+rank processes itself before anything touches the GPU; a launcher whose WORLD_SIZE differs from
+--gpus, or a LOCAL_RANK without a GPU, ends the run with status 2. n_gpus is the world size the
+process group reports. A hung post-timing exchange ends every rank with status 3 after rank 0
+has printed the line.
 
 Fields beyond the driver contract:
   roofline     — dominant kernel (AES-GCM seal): algorithmic bytes per launch (2L+16 per record:
@@ -17,6 +21,9 @@ Fields beyond the driver contract:
                  achieved / copy_GBps.
   wire_GiBps   — (--wire) the same records sealed as one contiguous wire stream, header || ct ||
                  tag per record (ATLS_MODE_WIRE), payload GiB/s from HIP events.
+  open         — the decrypt half: open_batch over the sealed records of the same batch (GiB/s,
+                 kernel_ms from HIP events, roofline frac with the same 2L+16 bytes per record),
+                 statuses, lengths and (uniform configs) every plaintext byte checked.
   cpu_baseline — the oracle (literal C restatement of the reference's algorithm: byte S-box
                  AES with bit-serial MixColumns, bit-serial GHASH) on a bounded sample of the
                  same records, on this host: --cpu-threads threads (value) and 1 thread
@@ -33,8 +40,6 @@ sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
-
-from anothertls_amd import dist  # noqa: E402
 
 METRIC = "GiB/s device-resident TLS-record AEAD (16 KiB recs); % HBM roofline @1/2/4/8 GPU"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
@@ -60,7 +65,25 @@ def parse():
                    help="N > 1: skip the sharded scatter / seal / gather of rank 0's batch")
     p.add_argument("--scatter-timeout", type=float, default=120.0,
                    help="N > 1: seconds the sharded exchange may take before the line is printed without it")
+    p.add_argument("--no-open", action="store_true", help="skip the open (decrypt) half of the measurement")
+    p.add_argument("--dry-run", action="store_true",
+                   help="CPU only (gloo): the launcher, rendezvous, timing and JSON line with a stub sealer "
+                        "instead of the engine (tests of the N > 1 plumbing)")
     return p.parse_args()
+
+
+def cpu_model():
+    """The host CPU's model name (/proc/cpuinfo), for cpu_baseline."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
 
 
 def _oracle_rate(ora, okeys, recs, inbuf_host, n_rec, threads, budget_s):
@@ -93,7 +116,7 @@ def cpu_baseline(batch, inbuf_host, budget_s, threads):
     n_rec = min(len(recs), 4096)
     v1, d1, p1, t1 = _oracle_rate(ora, okeys, recs, inbuf_host, n_rec, 1, budget_s / 4)
     vn, dn, pn, tn = _oracle_rate(ora, okeys, recs, inbuf_host, n_rec, threads, budget_s)
-    return dict(value=vn, unit="GiB/s", cores=threads, kind="port", value_1thread=v1,
+    return dict(value=vn, unit="GiB/s", cores=threads, cpu_model=cpu_model(), kind="port", value_1thread=v1,
                 sample=f"{dn} record seals ({pn} B AEAD payload) cycling over the first {n_rec} records of the same "
                        f"batch, oracle/ref_restatement.c ora_seal_batch, {threads} threads, {tn:.1f} s; 1 thread: "
                        f"{d1} records ({p1} B) in {t1:.1f} s")
@@ -105,7 +128,7 @@ def sharded_exchange(args, eng, dev, d_in, d_aux, d_ref_out, d_ref_tags, reps=3)
     Returns (rank 0) GiB/s of AEAD payload for scatter + seal + gather, max time over ranks, and
     whether the gathered bytes equal rank 0's single-GPU result."""
     import anothertls_amd as atls
-    from anothertls_amd import workload
+    from anothertls_amd import dist, workload
 
     b0 = workload.shard_batch(args.config, 0, n=args.records, n_keys=args.key_slots)  # same on every rank
     rank = dist.env_ranks()[0]
@@ -188,20 +211,77 @@ def run_c1(args):
                          "suite": "TLS_AES_128_GCM_SHA256", "path": "anothertls_amd.stream.StreamBatch (WIRE mode)"}}
     if not args.no_cpu_baseline:
         t = c1_cpu_reference(body, 1)
-        result["cpu_baseline"] = {"value": round(len(body) / t / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+        result["cpu_baseline"] = {"value": round(len(body) / t / 1e6, 3), "unit": "MB/s", "cores": 1,
+                                  "cpu_model": cpu_model(), "kind": "port",
                                   "sample": "one 1 MiB body (64 records) through the same socket loop, oracle "
                                             "ora_record_seal / ora_record_open per record"}
     print(json.dumps(result), flush=True)
+
+
+def run_dry(args):
+    """--dry-run: this rank's part of an N-rank job on the CPU (gloo) with a stub sealer (a byte XOR
+    over a small C2-shaped shard) in place of the engine -- the launcher, rendezvous, barrier +
+    max-over-ranks timing and the JSON line of the real run, without a GPU (tests/test_bench_launch.py)."""
+    from anothertls_amd import dist, workload
+
+    rank, _, world = dist.env_ranks()
+    dist.init("gloo")
+    batch = workload.shard_batch(args.config, rank, n=args.records or 64)
+    buf = np.random.default_rng(rank).integers(0, 256, batch["in_bytes"], dtype=np.uint8)
+    out = np.empty_like(buf)
+
+    def step():
+        np.bitwise_xor(buf, 0x5A, out=out)
+
+    wall = dist.timed_steps(step, args.steps, args.warmup, lambda: None)
+    ranks = dist.world_size()
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(dist.whole_job_rate(batch["payload"], args.steps, wall, ranks), 3),
+                          "unit": "GiB/s", "n_gpus": ranks, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+                          "dry_run": True, "config": {"workload": args.config, "records_per_gpu": len(batch["recs"])}}),
+              flush=True)
+    dist.close()
+
+
+def open_descs(recs):
+    """Open descriptors for the sealed records of a TLS-mode batch: each reads its ciphertext
+    (content || type, len + 1 bytes) at the seal's out_off and writes the inner plaintext back to
+    the same offset of a separate buffer (RecordPayloadProtection::decrypt, record.rs:201-240)."""
+    o = recs.copy()
+    o["in_off"] = recs["out_off"]
+    o["len"] = recs["len"] + 1
+    return o
 
 
 def main():
     args = parse()
     if args.config == C1:
         return run_c1(args)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # --gpus N without a launcher: one fresh process per GPU, as torch.distributed.run would start
+        # them; this process has not touched the GPU (nor loaded the engine) and only waits for them
+        from anothertls_amd import dist
+
+        sys.exit(dist.launch_ranks([os.path.abspath(__file__), *sys.argv[1:]], args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f"bench.py: WORLD_SIZE={env_world} from the launcher but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.dry_run:
+        return run_dry(args)
+    from anothertls_amd import dist
+
     rank, local, world = dist.env_ranks()
+    ndev = torch.cuda.device_count()  # does not initialise the GPU
+    if local >= ndev:
+        print(f"bench.py: LOCAL_RANK {local} but {ndev} visible GPU(s)", file=sys.stderr, flush=True)
+        sys.exit(2)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     dist.init("nccl", dev)
+    world = dist.world_size()  # as the process group reports it
 
     import anothertls_amd as atls
     from anothertls_amd import workload
@@ -253,6 +333,42 @@ def main():
     alg_bytes = 2 * payload + 16 * n
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
 
+    # ---- the decrypt half (Gcm::decrypt, gcm.rs:142-157, via record.rs:201-240) over the records
+    # just sealed: same records, same bytes per record (read L + 16-byte tag, write L) ----
+    opened = None
+    if not args.no_open:
+        orecs = open_descs(recs)
+        d_orecs = torch.from_numpy(orecs.view(np.uint8).copy()).to(dev)
+        d_pt = torch.zeros(batch["out_bytes"], dtype=torch.uint8, device=dev)
+        d_res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        q_recs, q_pt, q_res = d_orecs.data_ptr(), d_pt.data_ptr(), d_res.data_ptr()
+        o0, o1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for i in range(args.warmup + args.steps):
+            if i == args.warmup:
+                o0.record(stream)
+            eng.open_batch(q_recs, p_out, p_aux, p_tags, q_pt, q_res, flags=flags, n=n)
+        o1.record(stream)
+        sync()
+        open_ms = o0.elapsed_time(o1) / args.steps
+        res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
+        ok = bool((res["status"] == 0).all() and (res["content_len"] == recs["len"]).all()
+                  and (res["content_type"] == 23).all())
+        lens = recs["len"]
+        if ok and (lens == lens[0]).all() and (np.diff(recs["in_off"]) == recs["in_off"][1] - recs["in_off"][0]).all() \
+                and (np.diff(recs["out_off"]) == recs["out_off"][1] - recs["out_off"][0]).all():
+            # uniform records (C2-C4): every plaintext byte of every record against the sealed input
+            L, si, so = int(lens[0]), int(recs["in_off"][1] - recs["in_off"][0]), int(recs["out_off"][1] - recs["out_off"][0])
+            ok = bool(torch.equal(d_pt[: n * so].view(n, so)[:, :L], d_in[: n * si].view(n, si)[:, :L]))
+        open_alg = alg_bytes  # read L+1 ciphertext + 16 tag, write L+1 plaintext per record
+        open_ach = open_alg / (open_ms * 1e-3) / 1e9
+        opened = {"GiBps": round(payload / (open_ms * 1e-3) / 2**30, 3), "kernel_ms": round(open_ms, 4),
+                  "achieved_GBps": round(open_ach, 1), "frac": round(open_ach / HBM_PEAK_GBPS, 4),
+                  "plaintext_and_status_ok": ok,
+                  "what": "open_batch over the sealed records (device-resident, same batch), HIP events on the "
+                          "engine stream over the timed steps"}
+        del d_orecs, d_pt, d_res
+
     # measured on-device copy bandwidth: read + write of this batch's payload buffer
     d_cp = torch.empty_like(d_in)
     c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -296,6 +412,8 @@ def main():
                          "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes,
                          "copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(achieved / copy_gbps, 4)},
         }
+        if opened is not None:
+            result["open"] = opened
         if world == 1 and not args.no_cpu_baseline:
             sample = min(n, 4096)
             h_in = d_in[: int(recs["in_off"][sample - 1]) + int(recs["len"][sample - 1]) + 16].cpu().numpy()
@@ -331,9 +449,9 @@ def main():
         # over all ranks, scattered over RCCL, sealed by every rank's engine and gathered back
         # (dist.seal_sharded); reported beside `value`, which is the pre-sharded rate. The result
         # must equal rank 0's own single-GPU seal of the same records (d_out / d_tags above).
-        # The bench line must survive a failed or hung exchange: errors are caught, and a
-        # watchdog on every rank ends the process after --scatter-timeout s, rank 0 first
-        # printing the line without the exchange.
+        # A failed exchange is recorded in the line; a hung one fires the watchdog on every rank,
+        # rank 0 first printing the line without it, and the process exits non-zero
+        # (dist.WATCHDOG_EXIT): the measured line survives, and the status says something hung.
         def give_up():
             if rank == 0 and result is not None:
                 result["sharded_from_rank0"] = {"error": f"no result within {args.scatter_timeout:.0f} s"}
@@ -343,16 +461,17 @@ def main():
             lambda: sharded_exchange(args, eng, dev, d_in if rank == 0 else None, d_aux,
                                      d_out if rank == 0 else None, d_tags if rank == 0 else None),
             args.scatter_timeout, give_up)
-        if not ok:  # the bench line must survive a collective failure
+        if not ok:
             print(f"sharded exchange failed: {sg}", file=sys.stderr, flush=True)
-            sg = {"error": str(sg)[:200]}
+            sg = {"error": str(sg)[:200]}  # recorded in the line; the measured value stands
         if rank == 0 and result is not None:
             result["sharded_from_rank0"] = sg
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
     dist.close()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -2,7 +2,8 @@
 consecutive records and runs them 2 lanes per record when all are tiny (<= ATLS_CHACHA_TINY = 2048
 B), else 4 lanes per record in two rounds when all are short (<= ATLS_CHACHA_SHORT = 4096 B), else
 16 lanes per record in eight rounds (the third case below puts one long record among short ones,
-so two widths run in one launch); all are
+so two widths run in one launch); a batch of at most ATLS_CHACHA_LAT_MAX = 32 records (the single
+call) runs one record per wave at 64 lanes (chacha_kernel_lat, the fourth case); all are
 checked against the oracle on the lengths that exercise the per-lane Poly1305 combine and the
 reference's F4 quirk (ChaCha20::encrypt leaves the last block unencrypted when len % 64 == 0,
 crypto/chacha20/cipher.rs:99-102), sealed and reopened, with tampered tags."""
@@ -26,8 +27,8 @@ def atls():
     return a
 
 
-@pytest.mark.parametrize("lens", [TINY * 20, SHORT * 20, SHORT * 20 + [16384]],
-                         ids=["all-tiny-2-lanes", "all-short-4-lanes", "one-long-16-lanes"])
+@pytest.mark.parametrize("lens", [TINY * 20, SHORT * 20, SHORT * 20 + [16384], SHORT + [16383, 16384, 5000]],
+                         ids=["all-tiny-2-lanes", "all-short-4-lanes", "one-long-16-lanes", "few-records-64-lanes"])
 def test_chacha_widths_vs_oracle(atls, lens):
     from anothertls_amd import workload
 

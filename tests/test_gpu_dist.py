@@ -3,8 +3,12 @@
 * atls_multi_* (MultiEngine): a batch split by cumulative bytes over several engines, scattered,
   sealed / opened and gathered, equals one engine's result byte for byte (bytes between records
   included), for device-resident and host buffers, TLS and WIRE records, and tampered-tag opens.
-  With a repeated device the transport is device-to-device copies; distinct GPUs use RCCL (the
-  same code path around it; not exercisable on a one-GPU box).
+  With a repeated device the transport is device-to-device copies; distinct GPUs use RCCL. The
+  RCCL branch itself runs here too: ATLS_MULTI_RCCL_SELF=1 with device 0 repeated makes a one-rank
+  communicator through the product's rccl() loader, and every part's scatter / gather is a grouped
+  send / recv of rank 0 to itself (the same run_device code as between distinct GPUs).
+  Descriptors the engines would refuse are refused before anything is queued, and leave no
+  sticky error behind.
 * dist.seal_sharded with the real engine in two ranks (gloo, both on device 0): the batch at
   rank 0 is scattered, each rank's engine seals its range, and the gathered result equals the
   unsharded batch.
@@ -41,12 +45,16 @@ def _single_seal(b, inbuf, recs=None, out_bytes=None):
     return out, tags
 
 
-@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
-def test_multi_engine_device_buffers_equal_single_engine(devices):
+@pytest.mark.parametrize("devices,rccl_self", [([0], False), ([0, 0], False), ([0, 0, 0], False), ([0, 0], True),
+                                               ([0, 0, 0, 0], True)],
+                         ids=["1-copy", "2-copy", "3-copy", "2-rccl-self", "4-rccl-self"])
+def test_multi_engine_device_buffers_equal_single_engine(devices, rccl_self, monkeypatch):
     b, inbuf = _batch()
     ref_out, ref_tags = _single_seal(b, inbuf)
+    if rccl_self:
+        monkeypatch.setenv("ATLS_MULTI_RCCL_SELF", "1")
     m = atls.MultiEngine(devices)
-    assert not m.uses_rccl  # repeated / single device: copies
+    assert m.uses_rccl == rccl_self  # repeated device: copies, or RCCL rank 0 to itself
     m.set_keys(b["keys"])
     dev = torch.device("cuda", 0)
     d_in = torch.from_numpy(inbuf).to(dev)
@@ -207,3 +215,35 @@ def test_multi_engine_edge_cases_raw_records_and_wire_open():
         assert pt[o:o + L].tobytes() == inbuf[s:s + L].tobytes(), i
     m.close()
     e.close()
+
+
+@pytest.mark.parametrize("rccl_self", [False, True])
+def test_multi_engine_refuses_before_queueing(rccl_self, monkeypatch):
+    """A descriptor the engines would refuse (key slot past the table, unknown mode, no tag array
+    for a non-WIRE record) fails the whole batch with ILLEGAL_PARAMETER before anything is queued:
+    the caller's output is untouched, and the next good batch reports no stale error."""
+    if rccl_self:
+        monkeypatch.setenv("ATLS_MULTI_RCCL_SELF", "1")
+    b, inbuf = _batch(600)
+    m = atls.MultiEngine([0, 0, 0])
+    m.set_keys(b["keys"])
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(inbuf).to(dev)
+    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+    d_tags = torch.zeros(16 * len(b["recs"]), dtype=torch.uint8, device=dev)
+    for field, value in (("key_slot", len(b["keys"])), ("mode", 7)):
+        bad = b["recs"].copy()
+        bad[550][field] = value  # in the last part's range
+        d_out = torch.full((b["out_bytes"] + 16,), 0x5A, dtype=torch.uint8, device=dev)
+        with pytest.raises(atls.TlsError) as e:
+            m.seal_batch(bad, d_in, d_aux, d_out, d_tags, flags=atls.FLAG_DEVICE_PTRS)
+        assert e.value.code == 47
+        assert bool((d_out == 0x5A).all())  # nothing ran
+    with pytest.raises(atls.TlsError) as e:  # TLS records need a tag array
+        m.seal_batch(b["recs"], d_in, d_aux, d_out, None, flags=atls.FLAG_DEVICE_PTRS)
+    assert e.value.code == 47
+    ref_out, ref_tags = _single_seal(b, inbuf)
+    d_out = torch.full((b["out_bytes"] + 16,), 0x5A, dtype=torch.uint8, device=dev)
+    m.seal_batch(b["recs"], d_in, d_aux, d_out, d_tags, flags=atls.FLAG_DEVICE_PTRS)  # no stale error
+    assert np.array_equal(d_out.cpu().numpy(), ref_out) and np.array_equal(d_tags.cpu().numpy(), ref_tags)
+    m.close()

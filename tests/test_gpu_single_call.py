@@ -1,6 +1,8 @@
 """The Cipher-trait drop-in (atls_seal / atls_open) as the reference's record layer uses it: one
 call per record, from any thread (Arc<dyn Cipher + Send + Sync>, crypto/ciphersuite.rs:78-87,
-net/record.rs:191-193): concurrent calls from several threads, the per-thread key cache across
+net/record.rs:191-193): concurrent calls from several threads (more threads than the bounded pool of
+call contexts, ATLS_SINGLE_CONTEXTS = 8), records read in place from mapped pinned memory (up to
+4 KiB) and copied once (longer), the key cache across
 evictions, the ChaCha20 f32 block-count limit (chacha20/cipher.rs:94), and atls_update_keys."""
 import os
 import random
@@ -25,7 +27,8 @@ def _case(rng, keys):
     return suite, key, iv, aad, pt
 
 
-def test_concurrent_threads_vs_oracle():
+@pytest.mark.parametrize("n_threads", [8, 20])  # 20 > the 8 pooled contexts: callers wait for one
+def test_concurrent_threads_vs_oracle(n_threads):
     rng0 = random.Random(5)
     keys = [(s, bytes(rng0.getrandbits(8) for _ in range(kl))) for s, kl in
             [(0x1301, 16), (0x1301, 16), (0x1302, 32), (0x1301, 24), (0x1303, 32), (0x1303, 32)]]
@@ -47,7 +50,7 @@ def test_concurrent_threads_vs_oracle():
         except BaseException as exc:  # noqa: BLE001 -- reported by the main thread
             errors.append(exc)
 
-    threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
     for th in threads:
         th.start()
     for th in threads:
