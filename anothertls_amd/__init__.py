@@ -26,7 +26,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ATLS_LIB") or os.path.join(_HERE, "libatls.so")  # ATLS_LIB: tuning variants
 
 if not os.path.exists(LIB_PATH):
-    raise ImportError(f"anothertls_amd: {LIB_PATH} is missing; build it with `python -m anothertls_amd._build`")
+    raise ImportError(f"anothertls_amd: {LIB_PATH} is missing; build it with `python anothertls_amd/_build.py`")
 
 # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64 (same SONAME). If torch is
 # installed, load it first so libatls.so binds to that already-loaded runtime instead of pulling a
@@ -49,6 +49,7 @@ _lib.atls_engine_create.restype = _c.c_void_p
 _lib.atls_engine_create.argtypes = [_c.c_int]
 _lib.atls_engine_destroy.argtypes = [_c.c_void_p]
 _lib.atls_engine_sync.argtypes = [_c.c_void_p]
+_lib.atls_engine_join.argtypes = [_c.c_void_p]
 _lib.atls_engine_stream.restype = _c.c_void_p
 _lib.atls_engine_stream.argtypes = [_c.c_void_p]
 _lib.atls_set_keys.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32]
@@ -108,7 +109,7 @@ OPEN_RESULT_DTYPE = np.dtype([("content_len", "<u4"), ("status", "u1"), ("conten
 assert KEY_DTYPE.itemsize == 64 and REC_DTYPE.itemsize == 48 and OPEN_RESULT_DTYPE.itemsize == 8
 
 MODE_TLS, MODE_RAW, MODE_WIRE = 0, 1, 2
-FLAG_DEVICE_PTRS, FLAG_DEVICE_RECS, FLAG_NO_SYNC = 1, 2, 4
+FLAG_DEVICE_PTRS, FLAG_DEVICE_RECS, FLAG_NO_SYNC, FLAG_LAZY_JOIN = 1, 2, 4, 8
 
 
 class CipherSuite(enum.IntEnum):
@@ -285,6 +286,10 @@ class Engine:
 
     def sync(self):
         _check(_lib.atls_engine_sync(self._e))
+
+    def join(self):
+        """atls_engine_join: the engine stream waits for the side kernels of FLAG_LAZY_JOIN batches."""
+        _check(_lib.atls_engine_join(self._e))
 
     def set_keys(self, keys):
         keys = np.ascontiguousarray(keys, dtype=KEY_DTYPE)

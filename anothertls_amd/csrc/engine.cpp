@@ -86,7 +86,14 @@ struct atls_engine {
   bool has_aes = false, has_chacha = false;  // suites present in the key table: skip idle kernels
   int aes_nr_mask = 0;                       // bit 0/1/2: AES slots with 10/12/14 rounds
   DevBuf ks, t0, err, keys_stage, recs, in, out, aux, tags, res, secrets, dkeys;
-  DevBuf plan, plan_keys, plan_idx, plan_wg; // batch plan (plan.hip)
+  // Batch plans (plan.hip), two sets used by alternate planned batches: with ATLS_FLAG_LAZY_JOIN a
+  // batch's side kernel may still read its set while the next batch is planned into the other.
+  struct PlanSet {
+    DevBuf plan, keys, idx, wg;
+    hipEvent_t side_done = nullptr;  // the side (ChaCha20-Poly1305) kernel that read this set ended
+    bool pending = false;            // side_done recorded, not yet joined into the engine stream
+  } ps[2];
+  int par = 0, last_par = 0;  // set of the next / the last planned batch
   DevBuf grp_cnt, grp_aux, grp_idx;          // key groups of direct AES-GCM batches (plan.hip)
   uint32_t group_min = 2048;                 // ATLS_GCM_GROUP_MIN: smallest batch to group (0: never)
   int chacha_wgs = 8;                        // ATLS_CHACHA_WGS: ChaCha20-Poly1305 workgroups per CU
@@ -109,8 +116,19 @@ int take_err(atls_engine* e, uint32_t err) {
   return ATLS_ILLEGAL_PARAMETER;
 }
 
+// The engine stream waits for every side kernel not yet joined (ATLS_FLAG_LAZY_JOIN batches).
+int join_pending(atls_engine* e) {
+  for (auto& q : e->ps) {
+    if (!q.pending) continue;
+    if (hipStreamWaitEvent(e->stream, q.side_done, 0) != hipSuccess) return ATLS_INTERNAL_ERROR;
+    q.pending = false;
+  }
+  return ATLS_OK;
+}
+
 int finish(atls_engine* e, uint32_t flags) {
   if (flags & ATLS_FLAG_NO_SYNC) return ATLS_OK;
+  if (join_pending(e)) return ATLS_INTERNAL_ERROR;
   if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
   uint32_t err = 0;
   if (hipMemcpy(&err, e->err.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return ATLS_INTERNAL_ERROR;
@@ -148,9 +166,9 @@ int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n
   (void)slot;
   if (e->has_chacha)
     return atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, nullptr,
-                              e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s);
+                              nullptr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s);
   return atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
-                         (const uint32_t*)e->t0.p, nullptr, e->plan.p, (uint32_t*)e->err.p, e->n_slots,
+                         (const uint32_t*)e->t0.p, nullptr, nullptr, (uint32_t*)e->err.p, e->n_slots,
                          e->aes_nr_mask, nullptr, nullptr, e->cus, s);
 }
 
@@ -243,6 +261,8 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   hipStream_t s = e->stream;
   const bool dev_ptrs = flags & ATLS_FLAG_DEVICE_PTRS;
   const bool dev_recs = flags & ATLS_FLAG_DEVICE_RECS;
+  const bool lazy = (flags & ATLS_FLAG_LAZY_JOIN) && (flags & ATLS_FLAG_NO_SYNC) && dev_ptrs;
+  if (!lazy && join_pending(e)) return ATLS_INTERNAL_ERROR;  // a batch without the flag starts after all
   if (!dev_ptrs && dev_recs) return ATLS_ILLEGAL_PARAMETER;  // host buffers need host-visible descriptors
 
   // No tags array: every record must carry its tag in the wire record (ATLS_MODE_WIRE). The
@@ -298,14 +318,29 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   }
   int rc = 0;
   const uint32_t* idx = nullptr;
+  void* plan_hdr = nullptr;
+  auto& ps = e->ps[e->par];
   if (planned) {
-    if (!e->plan.reserve(sizeof(atls::PlanHdr)) || !e->plan_keys.reserve(n) || !e->plan_idx.reserve(4 * (size_t)n) ||
-        !e->plan_wg.reserve(2 * 4 * (size_t)atls::kPlanKeys * atls::kPlanMaxWG))
+    // this set was last read by the side kernel of the planned batch before the previous one: the
+    // plan waits for it on the device, or on the host if a buffer has to grow (a reallocation)
+    const size_t wg_bytes = 2 * 4 * (size_t)atls::kPlanKeys * atls::kPlanMaxWG;
+    const bool grow = ps.plan.cap < sizeof(atls::PlanHdr) || ps.keys.cap < n || ps.idx.cap < 4 * (size_t)n ||
+                      ps.wg.cap < wg_bytes;
+    if (ps.pending) {
+      if ((grow ? hipEventSynchronize(ps.side_done) : hipStreamWaitEvent(s, ps.side_done, 0)) != hipSuccess)
+        return ATLS_INTERNAL_ERROR;
+      ps.pending = false;
+    }
+    if (!ps.plan.reserve(sizeof(atls::PlanHdr)) || !ps.keys.reserve(n) || !ps.idx.reserve(4 * (size_t)n) ||
+        !ps.wg.reserve(wg_bytes))
       return ATLS_INTERNAL_ERROR;
-    rc = atls_launch_plan(open, e->ks.p, d_recs, n, e->n_slots, d_res, (uint32_t*)e->err.p, e->plan.p,
-                          (uint8_t*)e->plan_keys.p, (uint32_t*)e->plan_idx.p, (uint32_t*)e->plan_wg.p, e->cus, s);
+    rc = atls_launch_plan(open, e->ks.p, d_recs, n, e->n_slots, d_res, (uint32_t*)e->err.p, ps.plan.p,
+                          (uint8_t*)ps.keys.p, (uint32_t*)ps.idx.p, (uint32_t*)ps.wg.p, e->cus, s);
     if (rc) return rc;
-    idx = (const uint32_t*)e->plan_idx.p;
+    idx = (const uint32_t*)ps.idx.p;
+    plan_hdr = ps.plan.p;
+    e->last_par = e->par;
+    e->par ^= 1;
   }
   // Both suites present: ChaCha20-Poly1305 (VALU-bound) on the second stream beside AES-GCM
   // (LDS-bound), joined back into the engine stream.
@@ -318,9 +353,9 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
       cs = e->stream2;
     }
     rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, idx,
-                            e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs);
+                            plan_hdr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs);
     if (rc) return rc;
-    if (side && hipEventRecord(e->ev_side, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
+    if (side && hipEventRecord(ps.side_done, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
   if (e->has_aes) {
     // A direct batch large enough: records of one key slot go through the kernel in lane groups
@@ -343,11 +378,14 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
       ghdr = (const uint32_t*)((const uint8_t*)e->grp_aux.p + hdr_at);
     }
     rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
-                         (const uint32_t*)e->t0.p, idx, e->plan.p, (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask,
+                         (const uint32_t*)e->t0.p, idx, plan_hdr, (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask,
                          gidx, ghdr, e->cus, s);
   }
   if (rc) return rc;
-  if (side && hipStreamWaitEvent(s, e->ev_side, 0) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  if (side) {  // join now, or (lazy) when the set is reused / atls_engine_join / a batch without the flag
+    if (lazy) ps.pending = true;
+    else if (hipStreamWaitEvent(s, ps.side_done, 0) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  }
   if (!dev_ptrs) {
     if (out_end && hipMemcpyAsync(out, e->out.p, out_end, hipMemcpyDeviceToHost, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
@@ -375,6 +413,7 @@ int install_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t 
   int status = ATLS_OK;
   for (uint32_t i = 0; i < n && status == ATLS_OK; i++) status = key_status(keys[i]);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  if (join_pending(e)) return ATLS_INTERNAL_ERROR;  // no side kernel reads the table while it changes
   const uint32_t total = replace ? n : std::max(e->n_slots, first + n);
   const size_t need = sizeof(atls::KeySched) * (size_t)std::max<uint32_t>(total, 1);
   if (need > e->ks.cap) {  // grow, keeping the installed slots
@@ -555,13 +594,14 @@ int cached_slot(SingleCtx* c, uint16_t suite, const uint8_t* key, size_t key_len
 }
 
 // Records up to this many bytes are read by the kernel straight from the pinned staging block
-// (mapped host memory, no copy); longer ones are staged to the device in one copy (the kernel's
-// per-step loads over PCIe would cost more than the copy). Outputs always go straight to the
-// pinned block. ATLS_SINGLE_ZC_MAX overrides (tuning).
+// (mapped host memory, no copy); longer ones are staged to the device in one copy. Outputs always
+// go straight to the pinned block. Measured (profiles/r03/single_call_latency_zc*.json, median us
+// per call): 16,385-B AES-128-GCM seal 54.7 read in place vs 60.3 with the copy, 1,537 B 30 either
+// way. ATLS_SINGLE_ZC_MAX overrides (tuning).
 size_t single_zero_copy_max() {
   static const size_t v = [] {
     const char* e = std::getenv("ATLS_SINGLE_ZC_MAX");
-    return e ? (size_t)std::atol(e) : (size_t)4096;
+    return e ? (size_t)std::atol(e) : (size_t)1 << 20;
   }();
   return v;
 }
@@ -679,7 +719,11 @@ atls_engine* atls_engine_create(int device) {
       hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_plan, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&e->ev_side, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ps[0].side_done, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ps[1].side_done, hipEventDisableTiming) != hipSuccess) {
+    for (auto& q : e->ps)
+      if (q.side_done) (void)hipEventDestroy(q.side_done);
     if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);
     if (e->ev_side) (void)hipEventDestroy(e->ev_side);
     if (e->stream2) (void)hipStreamDestroy(e->stream2);
@@ -707,9 +751,12 @@ void atls_engine_destroy(atls_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   for (DevBuf* b : {&e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
-                    &e->secrets, &e->dkeys, &e->plan, &e->plan_keys, &e->plan_idx, &e->plan_wg,
-                    &e->grp_cnt, &e->grp_aux, &e->grp_idx})
+                    &e->secrets, &e->dkeys, &e->grp_cnt, &e->grp_aux, &e->grp_idx})
     b->release();
+  for (auto& q : e->ps) {
+    for (DevBuf* b : {&q.plan, &q.keys, &q.idx, &q.wg}) b->release();
+    if (q.side_done) (void)hipEventDestroy(q.side_done);
+  }
   if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);
   if (e->ev_side) (void)hipEventDestroy(e->ev_side);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
@@ -722,6 +769,13 @@ int atls_engine_sync(atls_engine* e) {
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
   return finish(e, 0);
+}
+
+int atls_engine_join(atls_engine* e) {
+  if (!e) return ATLS_INTERNAL_ERROR;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  return join_pending(e);
 }
 
 void* atls_engine_stream(atls_engine* e) { return e ? (void*)e->stream : nullptr; }
@@ -881,11 +935,12 @@ int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_
 
 // Debug: copy the last batch plan (PlanHdr words, then the first n_idx record indices) to host.
 extern "C" int atls_debug_plan(atls_engine* e, uint32_t* out, uint32_t n_idx) {
-  if (!e || !e->plan.p) return -1;
+  if (!e || !e->ps[e->last_par].plan.p) return -1;
   std::lock_guard<std::mutex> lk(e->mu);
-  if (!set_dev(e) || hipStreamSynchronize(e->stream) != hipSuccess) return -1;
-  if (hipMemcpy(out, e->plan.p, sizeof(atls::PlanHdr), hipMemcpyDeviceToHost) != hipSuccess) return -1;
-  if (n_idx && hipMemcpy(out + sizeof(atls::PlanHdr) / 4, e->plan_idx.p, 4 * (size_t)n_idx, hipMemcpyDeviceToHost) != hipSuccess)
+  const auto& q = e->ps[e->last_par];
+  if (!set_dev(e) || join_pending(e) || hipStreamSynchronize(e->stream) != hipSuccess) return -1;
+  if (hipMemcpy(out, q.plan.p, sizeof(atls::PlanHdr), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (n_idx && hipMemcpy(out + sizeof(atls::PlanHdr) / 4, q.idx.p, 4 * (size_t)n_idx, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return 0;
 }

@@ -1,24 +1,31 @@
-// AES-GCM seal/open for TLS records on gfx950 — the hot path of BASELINE.json's north star.
+// AES-GCM seal/open for TLS records on gfx950 -- the hot path of BASELINE.json's north star.
 //
 // Restates crypto/aes/gcm.rs:42-157 (Gcm::gcm, Cipher for Gcm) for a whole batch of
 // records, with the record-layer framing of net/record.rs:162-240 done on the device
 // (inner plaintext = content||type, 5-byte AAD header, nonce = static_iv ^ be64(seq)).
 //
-// Mapping: one record per wavefront (4 waves per workgroup, persistent grid-stride over
-// records). The record's GHASH input sequence is AAD blocks, ciphertext blocks, length
-// block; the wave walks "slots" s = 0..m where slot 0 computes E_K(J0) (gcm.rs:76) and
-// slot s >= 1 is GHASH block g = s-1. Lane l owns slots s = l (mod 64), so every 64-slot
-// step loads/stores one contiguous 1 KiB run of the record (coalesced 16 B per lane).
-//   * AES-CTR: T-table AES (one table, replicated 32x so each lane of a 32-lane LDS group
-//     reads its own bank: conflict-free ds_read_b32), counter block J0 + (b+1).
-//   * GHASH: lane-strided Horner with the fixed multiplier H^64, Y <- Y*H^64 ^ B, where the
-//     multiply is 32 lookups in a per-record 4-bit table in LDS (8 KiB per wave, built
-//     from x^(4p)*H^64, p = 0..31). A 4-bit position table (16 entries x 16 B) spans exactly
-//     one 256-B LDS bank row, so ds_read_b128 lookups never bank-conflict.
-//   * Lane combine: lane l's partial covers blocks whose last index leaves H^e
-//     (1 <= e <= 64) to go; Z_l = Y_l * H^e (bit-serial, per-lane e), XOR-reduced over the
-//     wave, tag = E_K(J0) ^ Z.
-// Bytes per record (roofline): read L, write L + 16 (tag) -- see DESIGN.md §Roofline.
+// Kernel gcm_kernel<OPEN, 12 waves, NR>: 12 waves per workgroup, one workgroup per CU (the LDS --
+// 64 KiB of T-tables + 8 KiB of GHASH table per wave = 160 KiB -- is what limits residency). A
+// record's GHASH input is AAD blocks, ciphertext blocks, length block; its "slots" are s = 0..m,
+// slot 0 = E_K(J0) (gcm.rs:76), slot s >= 1 = GHASH block s-1. Two ways to walk them:
+//   * gcm_record: one record per wave, lane l owns slots s = l (mod 64): each 64-slot step moves
+//     one contiguous 1 KiB run of the record (16 B per lane, coalesced). Per record: a GHASH table
+//     of H^64 built in LDS, the counter cache, the lane combine.
+//   * gcm_group (direct batches, key-grouped by plan.hip atls_launch_group): a run of 8 records of
+//     one key slot and one step count per wave, G lanes per record (G = 8 for AES-128, 16 for
+//     AES-192/256): lane gl of group g owns slots s = gl (mod G) of record g. One H^G table, one
+//     counter cache and one lane combine serve 64 / G records. Runs come from a work counter.
+// Per block:
+//   * AES-CTR: T-table rounds with two tables (T0, T1 = rotl8 T0) replicated 32x in LDS so lane l
+//     reads bank l & 31: conflict-free ds_read_b32. Counter-mode caching (Bernstein-Schwabe): a
+//     step's counters differ in byte 15 only, so rounds 1-2 take 5 lookups (133 per AES-128 block).
+//   * GHASH: lane-strided Horner Y <- Y * H^k ^ B (k = 64 or G) with a 4-bit table in LDS, 32
+//     positions x 16 entries x 16 B; a position is exactly one 256-B bank row, so the 32
+//     ds_read_b128 lookups never bank-conflict.
+//   * Lane combine: Z = sum_l Y_l * H^(e_l), e_l the powers each lane's last block still needs, by
+//     a transposed comb multiply, then a DPP + readlane XOR reduction; tag = E_K(J0) ^ Z.
+// Bytes per record (roofline): read L, write L + 16 (tag) -- see DESIGN.md §4. The LDS array is
+// the binding unit (394 array cycles per 64 blocks, ~75 % busy).
 #include <cstdlib>
 
 #include "gcm_common.h"

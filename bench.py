@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--scatter-timeout", type=float, default=120.0,
                    help="N > 1: seconds the sharded exchange may take before the line is printed without it")
     p.add_argument("--no-open", action="store_true", help="skip the open (decrypt) half of the measurement")
+    p.add_argument("--no-lazy-join", action="store_true",
+                   help="join a mixed batch's side kernel at the end of every step (A/B of ATLS_FLAG_LAZY_JOIN)")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU only (gloo): the launcher, rendezvous, timing and JSON line with a stub sealer "
                         "instead of the engine (tests of the N > 1 plumbing)")
@@ -299,7 +301,9 @@ def main():
     d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
     d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
     torch.cuda.synchronize(dev)
-    flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC
+    # LAZY_JOIN: a mixed batch's ChaCha20-Poly1305 kernel is not joined back at the end of each step,
+    # so the next step's plan and AES-GCM kernel start beside it (C5); no effect on one-suite batches
+    flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC | (0 if args.no_lazy_join else atls.FLAG_LAZY_JOIN)
     stream = torch.cuda.ExternalStream(eng.stream, device=dev)
 
     # raw device pointers: the buffers are resident and synchronized above, so no per-step wait
@@ -319,10 +323,12 @@ def main():
 
     def timed_step():
         if marks["n"] == args.warmup:
+            eng.join()  # the interval holds exactly the timed steps' kernels
             ev0.record(stream)
         step()
         marks["n"] += 1
         if marks["n"] == args.warmup + args.steps:
+            eng.join()
             ev1.record(stream)
 
     wall = dist.timed_steps(timed_step, args.steps, args.warmup, sync, dev)
@@ -346,8 +352,10 @@ def main():
         o0, o1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for i in range(args.warmup + args.steps):
             if i == args.warmup:
+                eng.join()
                 o0.record(stream)
             eng.open_batch(q_recs, p_out, p_aux, p_tags, q_pt, q_res, flags=flags, n=n)
+        eng.join()
         o1.record(stream)
         sync()
         open_ms = o0.elapsed_time(o1) / args.steps
@@ -439,8 +447,10 @@ def main():
         w0, w1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for i in range(args.warmup + args.steps):
             if i == args.warmup:
+                eng.join()
                 w0.record(stream)
             eng.seal_batch(d_wrecs.data_ptr(), d_in, d_aux, d_wout, None, flags=flags, n=n)
+        eng.join()
         w1.record(stream)
         sync()
         result["wire_GiBps"] = round(payload * args.steps / (w0.elapsed_time(w1) * 1e-3) / 2**30, 3)

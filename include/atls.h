@@ -80,9 +80,17 @@ enum {
   ATLS_FLAG_DEVICE_PTRS = 1u, /* in/aux/out/tags/results are device pointers (else host memory,
                                  staged through pinned buffers with async copies) */
   ATLS_FLAG_DEVICE_RECS = 2u, /* recs is a device pointer (keeps descriptors resident) */
-  ATLS_FLAG_NO_SYNC = 4u      /* return after enqueueing; call atls_engine_sync() before reading.
+  ATLS_FLAG_NO_SYNC = 4u,     /* return after enqueueing; call atls_engine_sync() before reading.
                                  A descriptor the device refuses (DEVICE_RECS) is then reported
-                                 as ATLS_ILLEGAL_PARAMETER by that atls_engine_sync. */
+                                 as ATLS_ILLEGAL_PARAMETER by that atls_engine_sync, or by any
+                                 later synchronous call on the engine (the error word is sticky
+                                 until a synchronous call reads it). */
+  ATLS_FLAG_LAZY_JOIN = 8u    /* with NO_SYNC and DEVICE_PTRS: a mixed-suite batch's ChaCha20-Poly1305
+                                 kernel (second stream) is not joined back into the engine stream
+                                 at the end of the batch; the next batch's plan and AES-GCM kernel
+                                 may start beside it. The engine stream covers it again after
+                                 atls_engine_join / atls_engine_sync or a batch without this flag.
+                                 Batches of one engine stay ordered per record kernel. */
 };
 
 /* One connection's write key (a "key slot"). 64 bytes. suite + key + static IV as produced by
@@ -140,8 +148,12 @@ int atls_open(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t*
 atls_engine* atls_engine_create(int device); /* NULL if the device is unusable */
 void atls_engine_destroy(atls_engine* e);
 int atls_engine_sync(atls_engine* e);
-/* HIP stream the engine launches on (hipStream_t as void*), for callers that time or order work. */
+/* HIP stream the engine launches on (hipStream_t as void*), for callers that time or order work.
+ * Work of ATLS_FLAG_LAZY_JOIN batches is on it only after atls_engine_join. */
 void* atls_engine_stream(atls_engine* e);
+/* Order the engine stream after every kernel of the batches issued so far (joins the side stream
+ * of ATLS_FLAG_LAZY_JOIN batches; no host wait). */
+int atls_engine_join(atls_engine* e);
 
 /* Install n key slots (host array). Runs the device key-setup kernel: AES round keys, H = E_K(0),
  * H^1..H^64 and the GHASH table seeds; ChaCha keys are used as given. Replaces previous slots. */

@@ -170,3 +170,63 @@ def test_sticky_error_reported_at_sync_and_cleared(atls):
         assert e.value.code == 47
         eng.seal_batch(d_good.data_ptr(), d_in, d_aux, d_out, d_tags, flags=flags, n=64)
         eng.close()
+
+
+def test_lazy_join_batches_equal_joined_batches(atls):
+    """ATLS_FLAG_LAZY_JOIN (mixed-suite batches leave their ChaCha20-Poly1305 kernel un-joined, the
+    two plan sets alternate): many back-to-back planned batches into different output buffers, with
+    a key-table update and an open in between, give exactly the joined batches' results; the
+    engine stream covers everything after atls_engine_join."""
+    import torch
+
+    from anothertls_amd import workload
+
+    b = workload.config_batch("c5_mixed_256Ki_x_64B-16KiB", n=3000)
+    n = len(b["recs"])
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    d_in = torch.randint(0, 256, (b["in_bytes"] + 16,), dtype=torch.uint8, device=dev, generator=g)
+    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+    d_recs = torch.from_numpy(b["recs"].view(np.uint8).copy()).to(dev)
+    ref = atls.Engine(0)
+    ref.set_keys(b["keys"])
+    r_out = torch.zeros(b["out_bytes"] + 16, dtype=torch.uint8, device=dev)
+    r_tags = torch.zeros(16 * n, dtype=torch.uint8, device=dev)
+    ref.seal_batch(d_recs.data_ptr(), d_in, d_aux, r_out, r_tags, flags=atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS, n=n)
+    eng = atls.Engine(0)
+    eng.set_keys(b["keys"])
+    torch.cuda.synchronize()
+    lazy = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC | atls.FLAG_LAZY_JOIN
+    outs = [torch.zeros_like(r_out) for _ in range(5)]
+    tags = [torch.zeros_like(r_tags) for _ in range(5)]
+    for _ in range(3):  # the same buffers again: the sets and the side stream are reused
+        for o, t in zip(outs, tags):
+            eng.seal_batch(d_recs.data_ptr(), d_in.data_ptr(), d_aux.data_ptr(), o.data_ptr(), t.data_ptr(), flags=lazy, n=n)
+    eng.join()
+    done = torch.cuda.Event()
+    done.record(torch.cuda.ExternalStream(eng.stream, device=dev))
+    done.synchronize()  # the engine stream alone now covers every kernel of those batches
+    for o, t in zip(outs, tags):
+        assert torch.equal(o, r_out) and torch.equal(t, r_tags)
+    # a key-table update after lazy batches waits for their side kernels (same keys: same results)
+    eng.seal_batch(d_recs.data_ptr(), d_in.data_ptr(), d_aux.data_ptr(), outs[0].data_ptr(), tags[0].data_ptr(),
+                   flags=lazy, n=n)
+    eng.update_keys(0, b["keys"][:5])
+    # open the lazily sealed records, lazily too, then a synchronous batch joins everything
+    orecs = b["recs"].copy()
+    orecs["in_off"], orecs["len"] = b["recs"]["out_off"], b["recs"]["len"] + 1
+    d_orecs = torch.from_numpy(orecs.view(np.uint8).copy()).to(dev)
+    d_pt = torch.zeros_like(r_out)
+    d_res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
+    eng.open_batch(d_orecs.data_ptr(), outs[0].data_ptr(), d_aux.data_ptr(), tags[0].data_ptr(), d_pt.data_ptr(),
+                   d_res.data_ptr(), flags=lazy, n=n)
+    eng.seal_batch(d_recs.data_ptr(), d_in, d_aux, outs[1], tags[1], flags=atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS, n=n)
+    res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
+    assert (res["status"] == 0).all() and (res["content_len"] == b["recs"]["len"]).all()
+    assert torch.equal(outs[0], r_out) and torch.equal(outs[1], r_out) and torch.equal(tags[1], r_tags)
+    h_in, h_pt = d_in.cpu().numpy(), d_pt.cpu().numpy()
+    for i in range(n):
+        o, s, L = int(b["recs"]["out_off"][i]), int(b["recs"]["in_off"][i]), int(b["recs"]["len"][i])
+        assert h_pt[o:o + L].tobytes() == h_in[s:s + L].tobytes(), i
+    eng.close()
+    ref.close()

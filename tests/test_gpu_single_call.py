@@ -2,7 +2,7 @@
 call per record, from any thread (Arc<dyn Cipher + Send + Sync>, crypto/ciphersuite.rs:78-87,
 net/record.rs:191-193): concurrent calls from several threads (more threads than the bounded pool of
 call contexts, ATLS_SINGLE_CONTEXTS = 8), records read in place from mapped pinned memory (up to
-4 KiB) and copied once (longer), the key cache across
+1 MiB) and copied once (longer), the key cache across
 evictions, the ChaCha20 f32 block-count limit (chacha20/cipher.rs:94), and atls_update_keys."""
 import os
 import random
