@@ -140,7 +140,13 @@ struct ChArgs {
   uint32_t n_slots;     // direct mode: key-table size
 };
 
-template <bool OPEN, int G>
+// LATE: r^2 and r^3 for the lane combine are recomputed after the slot loop instead of living
+// through it (10 fewer VGPRs there, 2 more multiplies per record and lane). Same-box A/B over 3
+// rounds (profiles/r03/ab_chacha_late_pow.log): the open kernels and the planned seal kernel spill
+// less (direct open 33 -> 17 VGPRs, planned open 57 -> 39, planned seal 5 -> 0): C5 open 0.350 ->
+// 0.323 ms, C5 seal 0.318 -> 0.316 ms, C3 open within noise; the direct seal kernel (no spills either
+// way) keeps them live (C3 seal 0.085-0.087 ms both ways).
+template <bool OPEN, int G, bool LATE>
 __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl) {
   // TLS and WIRE: nonce from (static IV, seq), 5-byte AAD; WIRE also frames the record
   const bool wire = d.mode == ATLS_MODE_WIRE;
@@ -193,6 +199,14 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   for (uint32_t base = 0; base <= jL; base += G) {
     const uint32_t j = base + (uint32_t)gl;
     const bool active = j <= jL;
+    // Latency path (G = 64, one record per wave, the single call): the block's data is loaded before
+    // its keystream is computed, so the load's latency (PCIe when the kernel reads pinned host
+    // memory) hides under the ChaCha rounds. The throughput paths keep the registers free instead.
+    uint4 pre[4] = {};
+    if (G == 64 && active && j >= 1 && j <= jmax && 64u * (j - 1) + 64u <= len) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) pre[q] = ld16(src + 64u * (j - 1) + 16 * q);
+    }
     uint32_t ks[16];
     if (active && j <= jmax) chacha_block(kw, j, nw, ks);
     if (base == 0) {
@@ -206,8 +220,8 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       r.l[3] = ((r2 >> 14) | (r3 << 18)) & M26;
       r.l[4] = r3 >> 8;
       rsq = p_mul(r, r);
-      rcu = p_mul(rsq, r);
       R = p_mul(rsq, rsq);  // r^4
+      if (!LATE) rcu = p_mul(rsq, r);
 #pragma unroll
       for (int d = 1; d < G; d <<= 1) {  // Hillis-Steele prefix product
         P130 t;
@@ -237,7 +251,32 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         cnt++;
       }
     } else {
-      uint32_t C[16];
+      // Horner of this slot's four 16-byte Poly1305 pieces (ciphertext, then the length block)
+      auto fold = [&](const uint32_t (&X)[16]) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t c = 4u * (j - 1) + u;
+          if (c < nct) {
+            if (u) inner = p_mul(inner, r);  // piece u = 0 starts the slot's Horner
+            p_add_block(inner, X[4 * u], X[4 * u + 1], X[4 * u + 2], X[4 * u + 3]);
+            cnt++;
+          } else if (c == nct) {  // le64(aad_len) || le64(ct_len) (poly1305.rs:63-64)
+            if (u) inner = p_mul(inner, r);
+            p_add_block(inner, tls ? 5u : aad_len, 0u, n, 0u);
+            cnt++;
+          }
+        }
+      };
+      // bytes past `valid` of a partial block are zero (the MAC's zero padding, the stores' mask)
+      auto mask_valid = [](uint32_t (&X)[16], uint32_t valid) {
+        if (valid < 64) {
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+            const int lo = 4 * q;
+            if ((int)valid < lo + 4) X[q] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - (int)valid)));
+          }
+        }
+      };
       if (j <= jmax) {
         const uint32_t off = 64u * (j - 1);
         uint32_t P[16];
@@ -245,7 +284,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         if (off + 64 <= len) {
 #pragma unroll
           for (int q = 0; q < 4; q++) {
-            const uint4 v = ld16(src + off + 16 * q);
+            const uint4 v = G == 64 ? pre[q] : ld16(src + off + 16 * q);
             P[4 * q] = v.x; P[4 * q + 1] = v.y; P[4 * q + 2] = v.z; P[4 * q + 3] = v.w;
           }
         } else {
@@ -259,60 +298,46 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
             }
           }
         }
-        const bool skip_xor = f4 && j == jmax;
+        const bool skip_xor = f4 && j == jmax;  // cipher.rs:99-102: the last block is not XORed
+        if (OPEN) {
+          // MAC over the received ciphertext first, then the plaintext in the same registers (no
+          // second 16-word block live beside the keystream: the open kernels stay within their caps)
+          mask_valid(P, valid);
+          fold(P);
 #pragma unroll
-        for (int q = 0; q < 16; q++) C[q] = skip_xor ? P[q] : (P[q] ^ ks[q]);
-        if (valid < 64) {
+          for (int q = 0; q < 16; q++) P[q] = skip_xor ? P[q] : (P[q] ^ ks[q]);
+          mask_valid(P, valid);
+        } else {
 #pragma unroll
-          for (int q = 0; q < 16; q++) {
-            const int lo = 4 * q;
-            if ((int)valid < lo + 4) C[q] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - (int)valid)));
-          }
+          for (int q = 0; q < 16; q++) P[q] = skip_xor ? P[q] : (P[q] ^ ks[q]);
+          mask_valid(P, valid);
         }
         if (valid == 64) {
 #pragma unroll
-          for (int q = 0; q < 4; q++) st16(dst + off + 16 * q, make_uint4(C[4 * q], C[4 * q + 1], C[4 * q + 2], C[4 * q + 3]));
+          for (int q = 0; q < 4; q++) st16(dst + off + 16 * q, make_uint4(P[4 * q], P[4 * q + 1], P[4 * q + 2], P[4 * q + 3]));
         } else {
 #pragma unroll
           for (int q = 0; q < 64; q++)
-            if ((uint32_t)q < valid) dst[off + q] = (uint8_t)(C[q >> 2] >> (8 * (q & 3)));
+            if ((uint32_t)q < valid) dst[off + q] = (uint8_t)(P[q >> 2] >> (8 * (q & 3)));
         }
         if (OPEN) {
           if (tls) {
             for (int q = 15; q >= 0; q--) {
-              if (C[q]) {
-                const int bi = 4 * q + (31 - __builtin_clz(C[q])) / 8;
-                lastnz = ((int64_t)(off + bi) << 8) | ((C[q] >> (8 * (bi & 3))) & 0xffu);
+              if (P[q]) {
+                const int bi = 4 * q + (31 - __builtin_clz(P[q])) / 8;
+                lastnz = ((int64_t)(off + bi) << 8) | ((P[q] >> (8 * (bi & 3))) & 0xffu);
                 break;
               }
             }
           }
-#pragma unroll
-          for (int q = 0; q < 16; q++) C[q] = P[q];  // MAC runs over the received ciphertext
-          if (valid < 64) {
-#pragma unroll
-            for (int q = 0; q < 16; q++) {
-              const int lo = 4 * q;
-              if ((int)valid < lo + 4) C[q] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - (int)valid)));
-            }
-          }
+        } else {
+          fold(P);  // seal: the MAC runs over the ciphertext just written
         }
       } else {
+        uint32_t Z[16];
 #pragma unroll
-        for (int q = 0; q < 16; q++) C[q] = 0;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint32_t c = 4u * (j - 1) + u;
-        if (c < nct) {
-          if (u) inner = p_mul(inner, r);  // piece u = 0 starts the slot's Horner
-          p_add_block(inner, C[4 * u], C[4 * u + 1], C[4 * u + 2], C[4 * u + 3]);
-          cnt++;
-        } else if (c == nct) {  // le64(aad_len) || le64(ct_len) (poly1305.rs:63-64)
-          if (u) inner = p_mul(inner, r);
-          p_add_block(inner, tls ? 5u : aad_len, 0u, n, 0u);
-          cnt++;
-        }
+        for (int q = 0; q < 16; q++) Z[q] = 0;
+        fold(Z);
       }
     }
     if (j == jL) {
@@ -338,7 +363,13 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       if (u == 0) { ru = p_zero(); ru.l[0] = 1; }
       P130 pw;
       if (c == 0) pw = ru;
-      else pw = p_mul(ru, c == 1 ? r : c == 2 ? rsq : rcu);
+      else {
+        if (LATE) {  // r^2, r^3 again here rather than live through the slot loop
+          rsq = p_mul(r, r);
+          rcu = p_mul(rsq, r);
+        }
+        pw = p_mul(ru, c == 1 ? r : c == 2 ? rsq : rcu);
+      }
       if (!(jf == 0 && na == 0)) contrib = p_mul(acc, pw);
     }
     if (l == jL % G) p_add(contrib, p_mul(innerL, r));
@@ -398,7 +429,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 
 // One group of G lanes seals / opens the record at work-list position q (direct batches: the
 // kernel validates the descriptor itself).
-template <bool OPEN, int G>
+template <bool OPEN, int G, bool LATE>
 __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W, uint32_t q, uint32_t cnt, int gl) {
   if (q >= cnt) return;
   const uint32_t r = W.record(q);
@@ -413,7 +444,7 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
       }
     }
   } else {
-    chacha_record<OPEN, G>(A, d, A.ks + d.key_slot, r, gl);
+    chacha_record<OPEN, G, LATE>(A, d, A.ks + d.key_slot, r, gl);
   }
 }
 
@@ -458,7 +489,7 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
   const uint32_t stride = gridDim.x * blockDim.x / 64u * kPer;
   for (uint32_t q0 = wave * kPer; q0 < cnt; q0 += stride)
-    chacha_group<OPEN, G>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
+    chacha_group<OPEN, G, true>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
 }
 
 // Records up to ATLS_CHACHA_TINY bytes (every record of a wave step) take ATLS_CHACHA_TINY_G
@@ -491,13 +522,13 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
     mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
     if (ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY) {
       constexpr int G = ATLS_CHACHA_TINY ? ATLS_CHACHA_TINY_G : 4;
-      chacha_group<OPEN, G>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
+      chacha_group<OPEN, G, OPEN>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
     } else if (mx <= (uint32_t)ATLS_CHACHA_SHORT) {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3);
+      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, OPEN>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3);
     } else {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15);
+      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, OPEN>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15);
     }
   }
 }
@@ -518,7 +549,7 @@ __global__ __launch_bounds__(256, PLANNED ? ATLS_CHACHA_MINW_SIDE : OPEN ? ATLS_
 template <bool OPEN>
 __global__ __launch_bounds__(64) void chacha_kernel_lat(ChArgs A) {
   const WorkList W{nullptr, nullptr, kListChacha, A.n};
-  chacha_group<OPEN, 64>(A, W, blockIdx.x, A.n, (int)(threadIdx.x & 63));
+  chacha_group<OPEN, 64, false>(A, W, blockIdx.x, A.n, (int)(threadIdx.x & 63));
 }
 
 }  // namespace atls

@@ -1,0 +1,87 @@
+// Latency floor of one Cipher-trait call on this box, through the C ABI (no Python): the median
+// microseconds of (a) an empty kernel launch + hipStreamSynchronize, (b) an empty kernel launch
+// whose one lane writes a flag into mapped pinned memory that the host spins on, (c) the same flag
+// written by hipStreamWriteValue32 behind the kernel, (d) atls_seal /
+// atls_open of one record (ChaCha20-Poly1305 and AES-128-GCM, 1,537 and 16,385 B). Prints JSON.
+// Build: hipcc --offload-arch=gfx950 -O2 -Iinclude tools/single_call_floor.hip -Lanothertls_amd -latls
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../include/atls.h"
+
+__global__ void empty_kernel(volatile uint32_t* flag, uint32_t v) {
+  if (flag && threadIdx.x == 0) {
+    __threadfence_system();
+    *flag = v;
+  }
+}
+
+template <typename F>
+double median_us(F f, int reps) {
+  f();
+  std::vector<double> t;
+  for (int i = 0; i < reps; i++) {
+    auto a = std::chrono::steady_clock::now();
+    f();
+    t.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count());
+  }
+  std::sort(t.begin(), t.end());
+  return t[t.size() / 2];
+}
+
+int main() {
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return 1;
+  uint32_t* flag = nullptr;
+  if (hipHostMalloc((void**)&flag, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return 1;
+  uint32_t* dflag = nullptr;
+  (void)hipHostGetDevicePointer((void**)&dflag, flag, 0);
+  *flag = 0;
+  const double sync_us = median_us([&] {
+    hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s, nullptr, 0u);
+    (void)hipStreamSynchronize(s);
+  }, 2000);
+  uint32_t it = 0;
+  const double spin_us = median_us([&] {
+    ++it;
+    hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s, dflag, it);
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != it) {
+    }
+  }, 2000);
+  (void)hipStreamSynchronize(s);
+  // (c) the flag written by the command processor after the kernel (hipStreamWriteValue32)
+  const double wv_us = median_us([&] {
+    ++it;
+    hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, s, nullptr, 0u);
+    if (hipStreamWriteValue32(s, dflag, it, 0) != hipSuccess) abort();
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != it) {
+    }
+  }, 2000);
+  (void)hipStreamSynchronize(s);
+  printf("{\"empty_launch_sync_us\": %.1f, \"empty_launch_flag_spin_us\": %.1f, \"empty_launch_writevalue_spin_us\": %.1f",
+         sync_us, spin_us, wv_us);
+  std::vector<uint8_t> key(32, 7), iv(12, 1), aad = {0x17, 3, 3, 0x06, 0x11}, tag(16);
+  for (uint16_t suite : {(uint16_t)ATLS_TLS_CHACHA20_POLY1305_SHA256, (uint16_t)ATLS_TLS_AES_128_GCM_SHA256}) {
+    const size_t kl = suite == ATLS_TLS_AES_128_GCM_SHA256 ? 16 : 32;
+    for (size_t n : {(size_t)1537, (size_t)16385}) {
+      std::vector<uint8_t> pt(n, 0x5a), ct(n), back(n);
+      const double seal = median_us([&] {
+        if (atls_seal(suite, key.data(), kl, iv.data(), 12, aad.data(), 5, pt.data(), n, ct.data(), tag.data())) abort();
+      }, 2000);
+      const double open = median_us([&] {
+        if (atls_open(suite, key.data(), kl, iv.data(), 12, aad.data(), 5, ct.data(), n, tag.data(), 16, back.data()))
+          abort();
+      }, 2000);
+      if (back != pt) abort();
+      printf(", \"%s_%zu_seal_us\": %.1f, \"%s_%zu_open_us\": %.1f", kl == 16 ? "aes128gcm" : "chacha20poly1305", n, seal,
+             kl == 16 ? "aes128gcm" : "chacha20poly1305", n, open);
+    }
+  }
+  printf("}\n");
+  return 0;
+}

@@ -1,0 +1,54 @@
+"""Diagnostic for HBM write / read amplification (run under rocprofv3 --pmc): seals a C3- or C2-shaped
+batch, device-resident, with a chosen output stride and key count, so FETCH / WRITE request counts can
+be compared between the config's packed layout (16-B aligned records) and line-aligned ones.
+python tools/traffic_probe.py --config c3 --out-align 128 --keys 4096 --steps 3"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--config", default="c3")
+    p.add_argument("--out-align", type=int, default=16)
+    p.add_argument("--in-align", type=int, default=16)
+    p.add_argument("--keys", type=int, default=4096)
+    p.add_argument("--steps", type=int, default=3)
+    a = p.parse_args()
+    import anothertls_amd as atls
+    from anothertls_amd import workload
+
+    name = {"c2": "c2_aes128gcm_64Ki_x_16KiB", "c3": "c3_chacha20poly1305_64Ki_x_1.5KiB"}[a.config]
+    b = workload.config_batch(name, n_keys=a.keys)
+    recs = b["recs"].copy()
+    n = len(recs)
+    L = recs["len"].astype(np.int64)
+    istr = (L[0] + a.in_align - 1) // a.in_align * a.in_align
+    ostr = (L[0] + 1 + a.out_align - 1) // a.out_align * a.out_align
+    recs["in_off"] = np.arange(n, dtype=np.uint64) * np.uint64(istr)
+    recs["out_off"] = np.arange(n, dtype=np.uint64) * np.uint64(ostr)
+    dev = torch.device("cuda", 0)
+    eng = atls.Engine(0)
+    eng.set_keys(b["keys"])
+    d_in = torch.randint(0, 256, (n * istr + 64,), dtype=torch.uint8, device=dev)
+    d_out = torch.empty(n * ostr + 64, dtype=torch.uint8, device=dev)
+    d_tags = torch.empty(16 * n, dtype=torch.uint8, device=dev)
+    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+    d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
+    torch.cuda.synchronize()
+    fl = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC
+    for _ in range(a.steps):
+        eng.seal_batch(d_recs.data_ptr(), d_in.data_ptr(), d_aux.data_ptr(), d_out.data_ptr(), d_tags.data_ptr(), flags=fl, n=n)
+    eng.sync()
+    print(f"{a.config} in stride {istr} out stride {ostr} keys {a.keys}: payload {int(L.sum()) + n} B per launch")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
