@@ -445,12 +445,8 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       }
       const v4u32 C = {P.x ^ st[0], P.y ^ st[1], P.z ^ st[2], P.w ^ st[3]};
       st16(dst + off, make_uint4(C.x, C.y, C.z, C.w));
+      if (OPEN && tls) lastnz = block_last_nz(C.x, C.y, C.z, C.w, off, lastnz);
       const v4u32 Bv = OPEN ? P : C;
-      if (OPEN && tls) {
-        const uint32_t cw[4] = {C.x, C.y, C.z, C.w};
-        const int j = last_nonzero(cw, 16);
-        if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((cw[j >> 2] >> (8 * (j & 3))) & 0xffu);
-      }
       ghash_mul<ATLS_GHASH_W>(y, wb);
       y[0] ^= Bv.x; y[1] ^= Bv.y; y[2] ^= Bv.z; y[3] ^= Bv.w;
 #ifdef ATLS_TT_STAMPS
@@ -773,11 +769,7 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
         const uint32_t D[4] = {Pv.x ^ sb[0], Pv.y ^ sb[1], Pv.z ^ sb[2], Pv.w ^ sb[3]};
         st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
         st16(dst + off2, make_uint4(D[0], D[1], D[2], D[3]));
-        if (OPEN) {  // the later block's last non-zero byte wins
-          const int j = last_nonzero(C, 16), j2 = last_nonzero(D, 16);
-          if (j2 >= 0) lastnz = ((int64_t)(off2 + j2) << 8) | ((D[j2 >> 2] >> (8 * (j2 & 3))) & 0xffu);
-          else if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((C[j >> 2] >> (8 * (j & 3))) & 0xffu);
-        }
+        if (OPEN) lastnz = block_last_nz(D[0], D[1], D[2], D[3], off2, block_last_nz(C[0], C[1], C[2], C[3], off, lastnz));
         ghash_mul<ATLS_GHASH_W>(y, wb);
         if (OPEN) { y[0] ^= Pu.x; y[1] ^= Pu.y; y[2] ^= Pu.z; y[3] ^= Pu.w; }
         else { y[0] ^= C[0]; y[1] ^= C[1]; y[2] ^= C[2]; y[3] ^= C[3]; }
@@ -799,10 +791,7 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
       else aes_rounds_tt<NR, 3>(st, rk, rkr, lb);
       const uint32_t C[4] = {Pu.x ^ st[0], Pu.y ^ st[1], Pu.z ^ st[2], Pu.w ^ st[3]};
       st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
-      if (OPEN) {
-        const int j = last_nonzero(C, 16);
-        if (j >= 0) lastnz = ((int64_t)(off + j) << 8) | ((C[j >> 2] >> (8 * (j & 3))) & 0xffu);
-      }
+      if (OPEN) lastnz = block_last_nz(C[0], C[1], C[2], C[3], off, lastnz);
       ghash_mul<ATLS_GHASH_W>(y, wb);
       if (OPEN) { y[0] ^= Pu.x; y[1] ^= Pu.y; y[2] ^= Pu.z; y[3] ^= Pu.w; }
       else { y[0] ^= C[0]; y[1] ^= C[1]; y[2] ^= C[2]; y[3] ^= C[3]; }

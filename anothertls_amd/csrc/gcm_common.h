@@ -191,6 +191,18 @@ __device__ __forceinline__ int last_nonzero(const uint32_t w[4], int valid) {
   return r;
 }
 
+// Content-type scan of one whole 16-byte plaintext block at byte offset off (record.rs:229-237):
+// (off + i) << 8 | byte for its last non-zero byte i, or prev when the block is all zero. Selects
+// only (no branch, no indexed register access), so it stays in the fast step's basic block.
+__device__ __forceinline__ int64_t block_last_nz(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t off,
+                                                 int64_t prev) {
+  const uint32_t x = w3 ? w3 : w2 ? w2 : w1 ? w1 : w0;
+  const uint32_t wi = w3 ? 12u : w2 ? 8u : w1 ? 4u : 0u;
+  const uint32_t bi = (31u - (uint32_t)__builtin_clz(x | 1u)) >> 3;  // x != 0 whenever it is used
+  const int64_t v = ((int64_t)(off + wi + bi) << 8) | ((x >> (8u * bi)) & 0xffu);
+  return x ? v : prev;
+}
+
 struct GcmArgs {
   const KeySched* ks;
   const atls_rec* recs;
