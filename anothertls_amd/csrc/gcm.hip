@@ -1016,7 +1016,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;
     if (ATLS_DBG_SHARED_GHASH && w == 16) return 16;
-    return (w == 4 || w == 8 || w == 12) ? w : 12;
+    return (w == 4 || w == 8 || w == 10 || w == 11 || w == 12) ? w : 12;
   }();
   uint32_t want = (n + waves - 1) / waves;
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
@@ -1031,7 +1031,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
     if (nr_mask & 2) { ATLS_LAUNCH_NR(W, 12) }         \
     if (nr_mask & 4) { ATLS_LAUNCH_NR(W, 14) }         \
   }
-  ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(12)
+  ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(10) ATLS_LAUNCH(11) ATLS_LAUNCH(12)
 #if ATLS_DBG_SHARED_GHASH
   ATLS_LAUNCH(16)
 #endif

@@ -134,9 +134,10 @@ typedef struct atls_engine atls_engine;
  * atls_seal  <- Cipher::encrypt: out = ciphertext (len B), tag = 16 B.
  * atls_open  <- Cipher::decrypt: out = plaintext (len B) or ATLS_BAD_RECORD_MAC (a tag of the
  *               wrong length is a mismatch, as `T != auth_tag` is in the reference).
- * Host pointers; device 0 or $ATLS_DEVICE. Reentrant and concurrent (Cipher is Send + Sync): each
- * calling thread has its own engines and streams, and keeps the device key schedules of its last
- * 16 keys per key size, so repeated keys cost no key setup (finished threads' contexts are reused). */
+ * Host pointers; device 0 or $ATLS_DEVICE. Reentrant and concurrent (Cipher is Send + Sync): a call
+ * leases one of at most $ATLS_SINGLE_CONTEXTS (8) call contexts -- engines, streams, a mapped pinned
+ * block the kernel reads and writes in place -- and callers beyond that wait for one; a context keeps
+ * the device key schedules of its last 16 keys per key size, so repeated keys cost no key setup. */
 int atls_seal(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
               const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, uint8_t* out,
               uint8_t tag[16]);

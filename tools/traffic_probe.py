@@ -20,6 +20,8 @@ def main():
     p.add_argument("--in-align", type=int, default=16)
     p.add_argument("--keys", type=int, default=4096)
     p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--raw", type=int, default=0,
+                   help="RAW-mode records of exactly this many bytes (no type byte: every 16-B / 64-B piece whole)")
     a = p.parse_args()
     import anothertls_amd as atls
     from anothertls_amd import workload
@@ -28,9 +30,16 @@ def main():
     b = workload.config_batch(name, n_keys=a.keys)
     recs = b["recs"].copy()
     n = len(recs)
+    aux = np.zeros(16, np.uint8)
+    if a.raw:  # RAW: nonce (12 B) || no AAD from aux for every record
+        recs["len"] = a.raw
+        recs["mode"] = atls.MODE_RAW
+        recs["iv_len"] = 12
+        recs["aad_len"] = 0
+        recs["aux_off"] = 0
     L = recs["len"].astype(np.int64)
     istr = (L[0] + a.in_align - 1) // a.in_align * a.in_align
-    ostr = (L[0] + 1 + a.out_align - 1) // a.out_align * a.out_align
+    ostr = (L[0] + (0 if a.raw else 1) + a.out_align - 1) // a.out_align * a.out_align
     recs["in_off"] = np.arange(n, dtype=np.uint64) * np.uint64(istr)
     recs["out_off"] = np.arange(n, dtype=np.uint64) * np.uint64(ostr)
     dev = torch.device("cuda", 0)
