@@ -138,6 +138,8 @@ struct ChArgs {
   PlanHdr* plan;
   uint32_t* err;        // direct mode: sticky error word
   uint32_t n_slots;     // direct mode: key-table size
+  uint32_t* done;       // one-record latency launch: completion flag (gcm_common.h signal_done)
+  uint32_t done_val;
 };
 
 // LATE: r^2 and r^3 for the lane combine are recomputed after the slot loop instead of living
@@ -550,6 +552,11 @@ template <bool OPEN>
 __global__ __launch_bounds__(64) void chacha_kernel_lat(ChArgs A) {
   const WorkList W{nullptr, nullptr, kListChacha, A.n};
   chacha_group<OPEN, 64, false>(A, W, blockIdx.x, A.n, (int)(threadIdx.x & 63));
+  if (A.done && A.n == 1u) {  // the single call's completion flag, after every store of the record
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // MI355X_MICROARCH.md: the compiler may drop it
+    if ((threadIdx.x & 63) == 0) __hip_atomic_store(A.done, A.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 }  // namespace atls
@@ -558,10 +565,10 @@ __global__ __launch_bounds__(64) void chacha_kernel_lat(ChArgs A) {
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
-                                  uint32_t n_slots, int grid, hipStream_t s) {
+                                  uint32_t n_slots, int grid, hipStream_t s, uint32_t* done, uint32_t done_val) {
   if (n == 0) return 0;
   atls::ChArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, idx,
-                 (atls::PlanHdr*)plan, err, n_slots};
+                 (atls::PlanHdr*)plan, err, n_slots, n == 1 ? done : nullptr, done_val};
   // the grid of the wider need (4 waves x 4 positions per workgroup at G = 16); the G = 4 path
   // strides over 16 positions per wave and simply finishes its list sooner
   const uint32_t want16 = (n + 15u) / 16u;

@@ -36,14 +36,14 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
-                               const uint32_t* ghdr, int grid, hipStream_t s);
+                               const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
 extern "C" size_t atls_group_hdr_offset(uint32_t n_slots);
 extern "C" int atls_launch_group(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt, void* aux,
                                  uint32_t* gidx, int cus, hipStream_t s);
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
-                                  uint32_t n_slots, int grid, hipStream_t s);
+                                  uint32_t n_slots, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
 extern "C" int atls_launch_hash(int op, uint32_t hl, const uint8_t* data, const atls_span* keys, const atls_span* msgs,
                                 uint32_t n, uint32_t out_len, uint8_t* out, hipStream_t s);
 extern "C" int atls_launch_key_schedule(uint32_t hl, const uint8_t* shared, uint32_t shared_len, const uint8_t* hello,
@@ -161,15 +161,14 @@ void extents(const atls_rec* recs, uint32_t n, bool open, size_t* in_end, size_t
 
 int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n, const uint8_t* d_in,
                    const uint8_t* d_aux, uint8_t* d_out, uint8_t* d_tags_out, const uint8_t* d_tags_in,
-                   atls_open_result* d_res, hipStream_t s, int slot) {
+                   atls_open_result* d_res, hipStream_t s, uint32_t* done = nullptr, uint32_t done_val = 0) {
   // direct batches only (one record kernel in the key table)
-  (void)slot;
   if (e->has_chacha)
     return atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, nullptr,
-                              nullptr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s);
+                              nullptr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s, done, done_val);
   return atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, nullptr, nullptr, (uint32_t*)e->err.p, e->n_slots,
-                         e->aes_nr_mask, nullptr, nullptr, e->cus, s);
+                         e->aes_nr_mask, nullptr, nullptr, e->cus, s, done, done_val);
 }
 
 // Host-memory batch (the socket path) in record chunks of ~kChunkBytes, alternating between the
@@ -228,7 +227,7 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
         hipMemcpyAsync(d_out + out_lo, (uint8_t*)out + out_lo, out_hi - out_lo, hipMemcpyHostToDevice, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     int rc = launch_records(e, open, d_recs + a, cnt, d_in, (const uint8_t*)e->aux.p, d_out, d_tags + 16 * (size_t)a,
-                            d_tags + 16 * (size_t)a, d_res + a, s, c);
+                            d_tags + 16 * (size_t)a, d_res + a, s);
     if (rc) return rc;
     if (pitched) {
       if (width && hipMemcpy2DAsync((uint8_t*)out + out_lo, pitch, d_out + out_lo, pitch, width, cnt,
@@ -353,7 +352,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
       cs = e->stream2;
     }
     rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, idx,
-                            plan_hdr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs);
+                            plan_hdr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs, nullptr, 0);
     if (rc) return rc;
     if (side && hipEventRecord(ps.side_done, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
@@ -379,7 +378,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     }
     rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, idx, plan_hdr, (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask,
-                         gidx, ghdr, e->cus, s);
+                         gidx, ghdr, e->cus, s, nullptr, 0);
   }
   if (rc) return rc;
   if (side) {  // join now, or (lazy) when the set is reused / atls_engine_join / a batch without the flag
@@ -475,6 +474,7 @@ struct SingleCtx {
   uint8_t* pin = nullptr;  // page-locked, mapped into the device's address space
   uint8_t* pin_dev = nullptr;
   size_t pin_cap = 0;
+  uint32_t calls = 0;  // completion-flag value of the last call (the flag word lives in the pinned block)
   bool reserve_pin(size_t n) {
     if (n <= pin_cap) return true;
     if (pin) (void)hipHostFree(pin);
@@ -639,8 +639,8 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
   uint32_t slot = 0;
   int rc = cached_slot(c, suite, key, key_len, &e, &slot);
   if (rc) return rc;
-  // pinned block: descriptor | tag | open result | iv || aad | input | output
-  const size_t rec_at = 0, tag_at = 64, res_at = 80, aux_at = 96;
+  // pinned block: descriptor | tag | open result | completion flag | iv || aad | input | output
+  const size_t rec_at = 0, tag_at = 64, res_at = 80, done_at = 88, aux_at = 96;
   const size_t in_at = (aux_at + iv_len + aad_len + 15) & ~size_t(15);
   const size_t out_at = (in_at + len + 15) & ~size_t(15), total = out_at + len + 16;
   if (!c->reserve_pin(total)) return ATLS_INTERNAL_ERROR;
@@ -675,10 +675,25 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
       return ATLS_INTERNAL_ERROR;
     src = (const uint8_t*)e->in.p;
   }
+  const uint32_t done_val = ++c->calls;
   rc = launch_records(e, open, (const atls_rec*)(src + rec_at), 1, src, src, hd, hd + tag_at, src + tag_at,
-                      (atls_open_result*)(hd + res_at), s, 0);
+                      (atls_open_result*)(hd + res_at), s, (uint32_t*)(hd + done_at), done_val);
   if (rc) return rc;
-  if (hipStreamSynchronize(s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  // spin on the kernel's completion flag (visible once every output byte is); a stream that ends
+  // without it (a fault) is reported by hipStreamQuery, checked every few thousand spins
+  const uint32_t* done = (const uint32_t*)(h + done_at);
+  for (uint64_t i = 1;; i++) {
+    if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == done_val) break;
+    if ((i & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipSuccess) {
+        if (__atomic_load_n(done, __ATOMIC_ACQUIRE) == done_val) break;
+        return ATLS_INTERNAL_ERROR;  // the launch ended and never signalled
+      }
+      if (q != hipErrorNotReady) return ATLS_INTERNAL_ERROR;
+    }
+    __builtin_ia32_pause();
+  }
   if (!open) {
     if (std::memcmp(h + tag_at, kTagCanary, 16) == 0) return ATLS_ILLEGAL_PARAMETER;
     if (len) std::memcpy(out, h + out_at, len);

@@ -948,6 +948,7 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   if (!A.gidx) {  // one record per wave, positions of the work list round-robin
     const uint32_t cnt = uni(W.size());
     for (uint32_t q = blockIdx.x * kWaves + wave; q < cnt; q += stride) gcm_one<NR, OPEN>(A, uni(W.record(q)), lb, wb, lane);
+    if (A.done && cnt == 1u && blockIdx.x == 0 && wave == 0) signal_done(A.done, A.done_val, lane);
     return;
   }
   // Key-grouped direct batch (plan.h): region B (records that form no lane group) round-robin
@@ -1002,21 +1003,22 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
 // nr_mask: bit 0/1/2 = key slots with 10/12/14 rounds exist (one launch each). plan/idx: the
 // batch plan of atls_launch_plan, or idx = nullptr for a direct batch (one round count only; the
 // kernel validates and reports through err). gidx/ghdr: a direct batch's key groups
-// (atls_launch_group) or nullptr. grid: workgroups per launch (one per CU).
+// (atls_launch_group) or nullptr. grid: workgroups per launch (one per CU). done / done_val: a
+// one-record direct launch signals completion there (the single call), else ignored.
 extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
-                               const uint32_t* ghdr, int grid, hipStream_t s) {
+                               const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val) {
   if (n == 0) return 0;
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, idx,
                   (atls::PlanHdr*)plan, err, n_slots, idx ? nullptr : gidx,
-                  (atls::GroupHdr*)const_cast<uint32_t*>(ghdr)};
+                  (atls::GroupHdr*)const_cast<uint32_t*>(ghdr), n == 1 ? done : nullptr, done_val};
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;
     if (ATLS_DBG_SHARED_GHASH && w == 16) return 16;
-    return (w == 4 || w == 8 || w == 10 || w == 11 || w == 12) ? w : 12;
+    return (w == 4 || w == 8 || w == 12) ? w : 12;
   }();
   uint32_t want = (n + waves - 1) / waves;
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
@@ -1031,7 +1033,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
     if (nr_mask & 2) { ATLS_LAUNCH_NR(W, 12) }         \
     if (nr_mask & 4) { ATLS_LAUNCH_NR(W, 14) }         \
   }
-  ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(10) ATLS_LAUNCH(11) ATLS_LAUNCH(12)
+  ATLS_LAUNCH(4) ATLS_LAUNCH(8) ATLS_LAUNCH(12)
 #if ATLS_DBG_SHARED_GHASH
   ATLS_LAUNCH(16)
 #endif

@@ -220,7 +220,18 @@ struct GcmArgs {
   uint32_t n_slots;        // direct mode: key-table size
   const uint32_t* gidx;    // direct mode: key groups (plan.hip atls_launch_group), or nullptr
   GroupHdr* ghdr;          // their region sizes and work counters
+  uint32_t* done;          // one-record direct launch (the single call): set to done_val when the
+  uint32_t done_val;       // record's outputs are visible system-wide (mapped host memory), or nullptr
 };
+
+// The single call's completion flag: after the wave's own stores have left (system-scope release),
+// one lane stores done_val into the caller's mapped host memory, where the host spins on it instead
+// of waiting for the launch's completion signal (tools/single_call_floor: 6.5 vs 11.9 us).
+__device__ __forceinline__ void signal_done(uint32_t* done, uint32_t val, int lane) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // MI355X_MICROARCH.md: the compiler may drop it
+  if (lane == 0) __hip_atomic_store(done, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Open result for one record (record.rs:203-240 decrypt + padding scan). lastnz = (position <<
 // 8 | byte) of the last non-zero plaintext byte, -1 if none.
