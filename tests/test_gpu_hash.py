@@ -100,3 +100,34 @@ def test_key_schedule_batch_vs_oracle():
         # the application secrets through the mirror's expand path agree with the chain's
         c, s = H.application_secrets(H.Hkdf.from_prk(ht, got[0][2]), fin[0])
         assert (c.pseudo_random_key, s.pseudo_random_key) == got[0][3:5]
+
+
+def test_hash_batch_spans_near_uint64_max_are_refused():
+    """A message or key span whose offset is close to 2^64 (off + len wraps) is refused with
+    ILLEGAL_PARAMETER before anything reaches the device (the bounds check no longer
+    wraps)."""
+    import hashlib
+
+    import numpy as np
+
+    import anothertls_amd as atls
+    from anothertls_amd import hash as H
+
+    lib = atls.library()
+    data = np.zeros(64, np.uint8)
+    out = np.zeros(64, np.uint8)
+    span = np.dtype([("off", "<u8"), ("len", "<u4"), ("reserved", "<u4")])
+    good = np.array([(0, 16, 0)], span)
+    for off, ln in [(2**64 - 8, 16), (2**64 - 1, 1), (65, 0), (60, 5)]:
+        bad = np.array([(off, ln, 0)], span)
+        for op, keys in [(0, None), (1, good)]:  # SHA (no keys), HMAC with a bad message span
+            rc = lib.atls_hash_batch(H._engine()._e, op, 32, data.ctypes.data, len(data),
+                                     None if keys is None else keys.ctypes.data, bad.ctypes.data, 1, 32,
+                                     out.ctypes.data)
+            assert rc == 47, (off, ln, op, rc)
+        rc = lib.atls_hash_batch(H._engine()._e, 1, 32, data.ctypes.data, len(data), bad.ctypes.data,
+                                 good.ctypes.data, 1, 32, out.ctypes.data)  # bad key span
+        assert rc == 47, (off, ln, rc)
+    ok = lib.atls_hash_batch(H._engine()._e, 0, 32, data.ctypes.data, len(data), None, good.ctypes.data, 1, 32,
+                             out.ctypes.data)
+    assert ok == 0 and bytes(out[:32]) == hashlib.sha256(bytes(16)).digest()
