@@ -20,6 +20,8 @@ def main():
     p.add_argument("--in-align", type=int, default=16)
     p.add_argument("--keys", type=int, default=4096)
     p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--in-shift", type=int, default=0, help="bytes added to every record's input offset")
+    p.add_argument("--out-shift", type=int, default=0, help="bytes added to every record's output offset")
     p.add_argument("--raw", type=int, default=0,
                    help="RAW-mode records of exactly this many bytes (no type byte: every 16-B / 64-B piece whole)")
     a = p.parse_args()
@@ -40,13 +42,13 @@ def main():
     L = recs["len"].astype(np.int64)
     istr = (L[0] + a.in_align - 1) // a.in_align * a.in_align
     ostr = (L[0] + (0 if a.raw else 1) + a.out_align - 1) // a.out_align * a.out_align
-    recs["in_off"] = np.arange(n, dtype=np.uint64) * np.uint64(istr)
-    recs["out_off"] = np.arange(n, dtype=np.uint64) * np.uint64(ostr)
+    recs["in_off"] = np.arange(n, dtype=np.uint64) * np.uint64(istr) + np.uint64(a.in_shift)
+    recs["out_off"] = np.arange(n, dtype=np.uint64) * np.uint64(ostr) + np.uint64(a.out_shift)
     dev = torch.device("cuda", 0)
     eng = atls.Engine(0)
     eng.set_keys(b["keys"])
-    d_in = torch.randint(0, 256, (n * istr + 64,), dtype=torch.uint8, device=dev)
-    d_out = torch.empty(n * ostr + 64, dtype=torch.uint8, device=dev)
+    d_in = torch.randint(0, 256, (n * istr + 64 + a.in_shift,), dtype=torch.uint8, device=dev)
+    d_out = torch.empty(n * ostr + 64 + a.out_shift, dtype=torch.uint8, device=dev)
     d_tags = torch.empty(16 * n, dtype=torch.uint8, device=dev)
     d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
     d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
