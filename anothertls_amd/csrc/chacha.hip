@@ -147,9 +147,20 @@ struct ChArgs {
 // rounds (profiles/r03/ab_chacha_late_pow.log): the open kernels and the planned seal kernel spill
 // less (direct open 33 -> 17 VGPRs, planned open 57 -> 39, planned seal 5 -> 0): C5 open 0.350 ->
 // 0.323 ms, C5 seal 0.318 -> 0.316 ms, C3 open within noise; the direct seal kernel (no spills either
-// way) keeps them live (C3 seal 0.085-0.087 ms both ways).
-template <bool OPEN, int G, bool LATE>
-__device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl) {
+// way) keeps them live (C3 seal 0.085-0.087 ms both ways; loading each slot's data before its keystream
+// measured 3-8 % slower on C3 in every variant, profiles/r03/ab_chacha_preload.log).
+// CARRY (direct batches; lds = this lane's 4 LDS slots of 16 B): a step of G lanes covers the record's
+// bytes [64 (base - 1), 64 (base + G - 1)), which starts 64 B before the slot grid, so unless the
+// output sits at (dst - 64) % 128 == 0 the window's last `mis` bytes share a 128-B line with the next
+// step's first bytes. Written at once, that line is written in two steps far apart and the L2 writes
+// it back twice (31 64-B writes per 24-segment record instead of 24.4, tools/_r3_traffic3.sh). With
+// CARRY those trailing 16-B pieces wait in LDS and are stored in the next step, beside the rest of
+// their line.
+typedef uint32_t v4u32_ch __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4u32_ch lds_uint4;
+template <bool OPEN, int G, bool LATE, bool CARRY = false>
+__device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl,
+                              lds_uint4* lds = nullptr) {
   // TLS and WIRE: nonce from (static IV, seq), 5-byte AAD; WIRE also frames the record
   const bool wire = d.mode == ATLS_MODE_WIRE;
   const bool tls = d.mode != ATLS_MODE_RAW;
@@ -197,6 +208,19 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   uint32_t sk[4] = {0, 0, 0, 0};
   P130 acc = p_zero(), innerL = p_zero();
   int64_t lastnz = -1;
+  const uint32_t mis = CARRY ? (uint32_t)((reinterpret_cast<uintptr_t>(dst) - 64u) & 127u) : 0u;
+  uint32_t cmask = 0, coff = 0;  // CARRY: pieces of the block at record offset coff waiting in LDS
+  auto flush = [&]() {
+    if (CARRY && cmask) {
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (cmask & (1u << q)) {
+          const v4u32_ch c = lds[q];
+          st16(dst + coff + 16 * q, make_uint4(c.x, c.y, c.z, c.w));
+        }
+      cmask = 0;
+    }
+  };
 
   for (uint32_t base = 0; base <= jL; base += G) {
     const uint32_t j = base + (uint32_t)gl;
@@ -314,9 +338,20 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
           for (int q = 0; q < 16; q++) P[q] = skip_xor ? P[q] : (P[q] ^ ks[q]);
           mask_valid(P, valid);
         }
+        flush();  // the previous step's trailing pieces go out with the rest of their line
         if (valid == 64) {
+          const uint32_t thr = 64u * (base + G - 1u) - mis;  // record offset where the window's partial line starts
 #pragma unroll
-          for (int q = 0; q < 4; q++) st16(dst + off + 16 * q, make_uint4(P[4 * q], P[4 * q + 1], P[4 * q + 2], P[4 * q + 3]));
+          for (int q = 0; q < 4; q++) {
+            const uint4 v = make_uint4(P[4 * q], P[4 * q + 1], P[4 * q + 2], P[4 * q + 3]);
+            if (CARRY && mis && off + 16u * q >= thr) {
+              lds[q] = v4u32_ch{v.x, v.y, v.z, v.w};
+              cmask |= 1u << q;
+              coff = off;
+            } else {
+              st16(dst + off + 16 * q, v);
+            }
+          }
         } else {
 #pragma unroll
           for (int q = 0; q < 64; q++)
@@ -350,6 +385,8 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     }
     (void)cnt;
   }
+
+  flush();
 
   // Lane partial: acc covers refs up to its last folded slot jf; contribution acc * r^(Q - ref).
   P130 contrib = p_zero();
@@ -431,8 +468,9 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 
 // One group of G lanes seals / opens the record at work-list position q (direct batches: the
 // kernel validates the descriptor itself).
-template <bool OPEN, int G, bool LATE>
-__device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W, uint32_t q, uint32_t cnt, int gl) {
+template <bool OPEN, int G, bool LATE, bool CARRY = false>
+__device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W, uint32_t q, uint32_t cnt, int gl,
+                                             lds_uint4* lds = nullptr) {
   if (q >= cnt) return;
   const uint32_t r = W.record(q);
   const atls_rec d = A.recs[r];
@@ -446,7 +484,7 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
       }
     }
   } else {
-    chacha_record<OPEN, G, LATE>(A, d, A.ks + d.key_slot, r, gl);
+    chacha_record<OPEN, G, LATE, CARRY>(A, d, A.ks + d.key_slot, r, gl, lds);
   }
 }
 
@@ -511,6 +549,8 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
 // Direct batch: P positions per wave and step, the width chosen per step from their longest record.
 template <bool OPEN>
 __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
+  __shared__ v4u32_ch carry[256 * 4];  // CARRY: 4 pieces of 16 B per lane (16 KiB per workgroup)
+  lds_uint4* lds = (lds_uint4*)(carry) + 4u * threadIdx.x;
   const WorkList W{nullptr, nullptr, kListChacha, A.n};
   const uint32_t cnt = A.n;
   constexpr uint32_t P = ATLS_CHACHA_TINY ? 64u / ATLS_CHACHA_TINY_G : 16u;
@@ -524,13 +564,13 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
     mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
     if (ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY) {
       constexpr int G = ATLS_CHACHA_TINY ? ATLS_CHACHA_TINY_G : 4;
-      chacha_group<OPEN, G, OPEN>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
+      chacha_group<OPEN, G, OPEN, true>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
     } else if (mx <= (uint32_t)ATLS_CHACHA_SHORT) {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, OPEN>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3);
+      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, OPEN, true>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3, lds);
     } else {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, OPEN>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15);
+      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, OPEN, true>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15, lds);
     }
   }
 }

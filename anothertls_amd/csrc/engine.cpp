@@ -614,8 +614,9 @@ constexpr uint32_t kTagCanary[4] = {0x6c1f9a3du, 0xb2e4570cu, 0x93d0e8a1u, 0x0f7
 
 // One Cipher::encrypt / decrypt call as a single RAW record: descriptor, tag, IV, AAD and input
 // are written into the context's pinned block, the kernel reads them there (or from one copy of
-// the block for long records) and writes output, tag and result straight back into it, and one
-// stream synchronisation ends the call. No other copy and no descriptor upload.
+// the block for long records), writes output, tag and result straight back into it and then a
+// completion flag the host spins on (no wait for the launch's completion signal). No other copy
+// and no descriptor upload.
 int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
            const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, const uint8_t* tag_in, size_t tag_len,
            uint8_t* out, uint8_t* tag_out) {

@@ -21,10 +21,10 @@ for round in 1 2 3; do
   done
 done
 if [ "${PMC:-1}" = 1 ]; then
-  CMD="python3 bench.py --config c2_aes128gcm_64Ki_x_16KiB --steps 5 --warmup 2 --no-cpu-baseline --no-open"
+  CMD="python3 bench.py --config ${PMC_CFG:-c2_aes128gcm_64Ki_x_16KiB} --steps 5 --warmup 2 --no-cpu-baseline --no-open"
   for lib in anothertls_amd/variants/libatls_*.so; do
     n=$(basename $lib .so)
-    ATLS_LIB=$PWD/$lib timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+    ATLS_LIB=$PWD/$lib timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY ${PMC_EXTRA:-SQ_WAIT_INST_LDS SQ_LDS_IDX_ACTIVE} SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
       -d gpurun_out/ab/pmc_$n -o run --output-format csv -- $CMD > gpurun_out/ab/pmc_$n.log 2>&1 || { echo "pmc $n rc=$?"; exit 1; }
     echo "pmc $n done"
   done
