@@ -546,6 +546,13 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
 #define ATLS_CHACHA_TINY_G 2
 #endif
 
+// CARRY on seals: C3 seal traffic 1.28x -> 1.11x of the algorithmic bytes but the kernel 0.0873 ->
+// 0.0905 ms (+3.7 %; 2 more spilled VGPRs); opens 0.1023 -> 0.1004 ms with traffic 1.47x -> 1.29x
+// (profiles/r03/ab_chacha_carry.log). The seal kernel is not HBM-bound, so carry stays on opens only.
+#ifndef ATLS_CHACHA_CARRY_SEAL
+#define ATLS_CHACHA_CARRY_SEAL 0
+#endif
+
 // Direct batch: P positions per wave and step, the width chosen per step from their longest record.
 template <bool OPEN>
 __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
@@ -564,13 +571,13 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
     mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
     if (ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY) {
       constexpr int G = ATLS_CHACHA_TINY ? ATLS_CHACHA_TINY_G : 4;
-      chacha_group<OPEN, G, OPEN, true>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
+      chacha_group<OPEN, G, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
     } else if (mx <= (uint32_t)ATLS_CHACHA_SHORT) {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, OPEN, true>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3, lds);
+      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3, lds);
     } else {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, OPEN, true>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15, lds);
+      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15, lds);
     }
   }
 }
