@@ -17,9 +17,9 @@ case ${1:-A} in
     run c1 300 python bench.py --config c1_server_https_loopback_1MiB --steps 20
     ;;
   B)
-    for c in c2:c2_aes128gcm_64Ki_x_16KiB c3:c3_chacha20poly1305_64Ki_x_1.5KiB c4:c4_aes256gcm_1Mi_x_16KiB c5:c5_mixed_256Ki_x_64B-16KiB; do
+    for c in ${CFGS:-c2:c2_aes128gcm_64Ki_x_16KiB c3:c3_chacha20poly1305_64Ki_x_1.5KiB c4:c4_aes256gcm_1Mi_x_16KiB c5:c5_mixed_256Ki_x_64B-16KiB}; do
       bash tools/profile_round.sh ${c#*:} ${c%%:*} || exit 1
     done
-    bash tools/pmc_stall.sh c2_aes128gcm_64Ki_x_16KiB || exit 1
+    [ -n "$CFGS" ] || bash tools/pmc_stall.sh c2_aes128gcm_64Ki_x_16KiB || exit 1
     ;;
 esac
