@@ -156,6 +156,17 @@ struct ChArgs {
 // it back twice (31 64-B writes per 24-segment record instead of 24.4, tools/_r3_traffic3.sh). With
 // CARRY those trailing 16-B pieces wait in LDS and are stored in the next step, beside the rest of
 // their line.
+// MAC_FIRST (opens; 1 = planned kernels, 2 = planned and direct): a data slot's ciphertext is folded
+// into the MAC before its keystream is computed, so the 16 keystream words are not live through the
+// Poly1305 products. Planned open kernel (128-VGPR cap) spills 128 -> 12 B per lane, direct open 68 ->
+// 28. The spills were HBM traffic: C5's ChaCha open read 2.23 M 128-B lines per launch (the seal 1.12
+// M) and wrote 3.07 M requests (2.22 M), now 1.13 M / 2.23 M. Same-box A/B over 3 rounds
+// (profiles/r03/ab_chacha_mac_first.log): C5 open kernel 0.320 -> 0.306 ms, C3 open 0.1010 -> 0.0994 ms;
+// a 3-wave bound for the planned open instead (152 VGPRs, no spills) fixed the traffic but not the
+// time (0.325 ms: no wave of it fits beside an AES-GCM workgroup).
+#ifndef ATLS_CHACHA_OPEN_MAC_FIRST
+#define ATLS_CHACHA_OPEN_MAC_FIRST 2
+#endif
 typedef uint32_t v4u32_ch __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4u32_ch lds_uint4;
 template <bool OPEN, int G, bool LATE, bool CARRY = false>
@@ -208,6 +219,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   uint32_t sk[4] = {0, 0, 0, 0};
   P130 acc = p_zero(), innerL = p_zero();
   int64_t lastnz = -1;
+  constexpr bool MAC_FIRST = OPEN && G != 64 && (CARRY ? ATLS_CHACHA_OPEN_MAC_FIRST >= 2 : ATLS_CHACHA_OPEN_MAC_FIRST >= 1);
   const uint32_t mis = CARRY ? (uint32_t)((reinterpret_cast<uintptr_t>(dst) - 64u) & 127u) : 0u;
   uint32_t cmask = 0, coff = 0;  // CARRY: pieces of the block at record offset coff waiting in LDS
   auto flush = [&]() {
@@ -234,7 +246,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       for (int q = 0; q < 4; q++) pre[q] = ld16(src + 64u * (j - 1) + 16 * q);
     }
     uint32_t ks[16];
-    if (active && j <= jmax) chacha_block(kw, j, nw, ks);
+    if (active && j <= jmax && (!MAC_FIRST || j == 0)) chacha_block(kw, j, nw, ks);
     if (base == 0) {
       // Poly1305 one-time key from block 0 (poly1305.rs:19-22), broadcast within the group.
       uint32_t r0 = __shfl(ks[0], 0, G), r1 = __shfl(ks[1], 0, G), r2 = __shfl(ks[2], 0, G), r3 = __shfl(ks[3], 0, G);
@@ -330,6 +342,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
           // second 16-word block live beside the keystream: the open kernels stay within their caps)
           mask_valid(P, valid);
           fold(P);
+          if (MAC_FIRST) chacha_block(kw, j, nw, ks);
 #pragma unroll
           for (int q = 0; q < 16; q++) P[q] = skip_xor ? P[q] : (P[q] ^ ks[q]);
           mask_valid(P, valid);
@@ -517,6 +530,9 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 #ifndef ATLS_CHACHA_MINW_SIDE
 #define ATLS_CHACHA_MINW_SIDE 4
 #endif
+#ifndef ATLS_CHACHA_MINW_SIDE_OPEN
+#define ATLS_CHACHA_MINW_SIDE_OPEN ATLS_CHACHA_MINW_SIDE
+#endif
 #ifndef ATLS_CHACHA_PLANNED_G
 #define ATLS_CHACHA_PLANNED_G 16  // lanes per record in planned (mixed) batches; C5 0.341 ms at 16, 0.359 at
                                   // 8, 0.435 at 4 (profiles/r02/ab_chacha_planned_g.log)
@@ -583,7 +599,7 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
 }
 
 template <bool OPEN, bool PLANNED>
-__global__ __launch_bounds__(256, PLANNED ? ATLS_CHACHA_MINW_SIDE : OPEN ? ATLS_CHACHA_MINW_OPEN : ATLS_CHACHA_MINW_SEAL) void chacha_kernel(ChArgs A) {
+__global__ __launch_bounds__(256, PLANNED ? (OPEN ? ATLS_CHACHA_MINW_SIDE_OPEN : ATLS_CHACHA_MINW_SIDE) : OPEN ? ATLS_CHACHA_MINW_OPEN : ATLS_CHACHA_MINW_SEAL) void chacha_kernel(ChArgs A) {
   const int lane = threadIdx.x & 63;
   if constexpr (PLANNED) chacha_batch<OPEN, ATLS_CHACHA_PLANNED_G>(A, lane);
   else chacha_direct<OPEN>(A, lane);
