@@ -28,25 +28,38 @@ struct P130 { uint32_t l[5]; };
 
 __device__ __forceinline__ P130 p_zero() { P130 z; for (int i = 0; i < 5; i++) z.l[i] = 0; return z; }
 
-// h * r mod p, partially reduced (limbs < 2^26 + small). Inputs: limbs < 2^27.
-__device__ __forceinline__ P130 p_mul(const P130& h, const P130& r) {
+// d += h * r (unreduced 64-bit column sums; 2^130 = 5 mod p folds the high columns back with 5 r).
+__device__ __forceinline__ void p_mac(uint64_t (&d)[5], const P130& h, const P130& r) {
   const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
   const uint64_t h0 = h.l[0], h1 = h.l[1], h2 = h.l[2], h3 = h.l[3], h4 = h.l[4];
-  uint64_t d0 = h0 * r.l[0] + h1 * s4 + h2 * s3 + h3 * s2 + h4 * s1;
-  uint64_t d1 = h0 * r.l[1] + h1 * r.l[0] + h2 * s4 + h3 * s3 + h4 * s2;
-  uint64_t d2 = h0 * r.l[2] + h1 * r.l[1] + h2 * r.l[0] + h3 * s4 + h4 * s3;
-  uint64_t d3 = h0 * r.l[3] + h1 * r.l[2] + h2 * r.l[1] + h3 * r.l[0] + h4 * s4;
-  uint64_t d4 = h0 * r.l[4] + h1 * r.l[3] + h2 * r.l[2] + h3 * r.l[1] + h4 * r.l[0];
+  d[0] += h0 * r.l[0] + h1 * s4 + h2 * s3 + h3 * s2 + h4 * s1;
+  d[1] += h0 * r.l[1] + h1 * r.l[0] + h2 * s4 + h3 * s3 + h4 * s2;
+  d[2] += h0 * r.l[2] + h1 * r.l[1] + h2 * r.l[0] + h3 * s4 + h4 * s3;
+  d[3] += h0 * r.l[3] + h1 * r.l[2] + h2 * r.l[1] + h3 * r.l[0] + h4 * s4;
+  d[4] += h0 * r.l[4] + h1 * r.l[3] + h2 * r.l[2] + h3 * r.l[1] + h4 * r.l[0];
+}
+
+// Column sums -> limbs (< 2^26, limb 1 < 2^26 + 2^8). The top carry times 5 is formed in 64 bits: with
+// up to four products summed (p_sop4) the carry out of column 4 reaches 2^31.
+__device__ __forceinline__ P130 p_red(uint64_t (&d)[5]) {
   P130 o;
   uint64_t c;
-  c = d0 >> 26; o.l[0] = (uint32_t)d0 & M26; d1 += c;
-  c = d1 >> 26; o.l[1] = (uint32_t)d1 & M26; d2 += c;
-  c = d2 >> 26; o.l[2] = (uint32_t)d2 & M26; d3 += c;
-  c = d3 >> 26; o.l[3] = (uint32_t)d3 & M26; d4 += c;
-  c = d4 >> 26; o.l[4] = (uint32_t)d4 & M26;
-  o.l[0] += (uint32_t)c * 5;
-  o.l[1] += o.l[0] >> 26; o.l[0] &= M26;
+  c = d[0] >> 26; o.l[0] = (uint32_t)d[0] & M26; d[1] += c;
+  c = d[1] >> 26; o.l[1] = (uint32_t)d[1] & M26; d[2] += c;
+  c = d[2] >> 26; o.l[2] = (uint32_t)d[2] & M26; d[3] += c;
+  c = d[3] >> 26; o.l[3] = (uint32_t)d[3] & M26; d[4] += c;
+  c = d[4] >> 26; o.l[4] = (uint32_t)d[4] & M26;
+  const uint64_t t = c * 5u + o.l[0];
+  o.l[0] = (uint32_t)t & M26;
+  o.l[1] += (uint32_t)(t >> 26);
   return o;
+}
+
+// h * r mod p, partially reduced (limbs < 2^26 + small). Inputs: limbs < 2^27.
+__device__ __forceinline__ P130 p_mul(const P130& h, const P130& r) {
+  uint64_t d[5] = {0, 0, 0, 0, 0};
+  p_mac(d, h, r);
+  return p_red(d);
 }
 
 // Add a full 16-byte block (raw LE words) plus 2^128 (poly1305.rs:39-43).
@@ -59,6 +72,31 @@ __device__ __forceinline__ void p_add_block(P130& h, uint32_t w0, uint32_t w1, u
 }
 
 __device__ __forceinline__ void p_add(P130& a, const P130& b) { for (int i = 0; i < 5; i++) a.l[i] += b.l[i]; }
+
+// A full data slot's MAC in one reduction (SOP): acc' = acc r^(4G) + c0 r^3 + c1 r^2 + c2 r + c3, the
+// four products summed as 64-bit column sums before one carry chain, instead of three Horner steps and
+// the slot step, each reduced (four carry chains). Column sums stay below 2^59 (p_red). The acc product
+// goes last so the data words die as they are folded. Same-box A/B over 3 rounds
+// (profiles/r03/ab_c3_w2.log): C3 seal kernel 0.0878 -> 0.0840 ms; with the acc product first it spilled
+// 19 VGPRs and measured 12 % slower (profiles/r03/ab_c3_sop_rot16.log).
+__device__ __forceinline__ void p_sop4(P130& acc, bool first, const P130& rG, const uint32_t (&X)[16],
+                                       const P130& r, const P130& rsq, const P130& rcu) {
+  uint64_t d[5];
+  P130 c = p_zero();
+  p_add_block(c, X[12], X[13], X[14], X[15]);
+  for (int i = 0; i < 5; i++) d[i] = c.l[i];
+  c = p_zero();
+  p_add_block(c, X[0], X[1], X[2], X[3]);
+  p_mac(d, c, rcu);
+  c = p_zero();
+  p_add_block(c, X[4], X[5], X[6], X[7]);
+  p_mac(d, c, rsq);
+  c = p_zero();
+  p_add_block(c, X[8], X[9], X[10], X[11]);
+  p_mac(d, c, r);
+  if (!first) p_mac(d, acc, rG);
+  acc = p_red(d);
+}
 
 __device__ __forceinline__ void p_carry(P130& h) {
   uint32_t c;
@@ -164,12 +202,15 @@ struct ChArgs {
 // (profiles/r03/ab_chacha_mac_first.log): C5 open kernel 0.320 -> 0.306 ms, C3 open 0.1010 -> 0.0994 ms;
 // a 3-wave bound for the planned open instead (152 VGPRs, no spills) fixed the traffic but not the
 // time (0.325 ms: no wave of it fits beside an AES-GCM workgroup).
+#ifndef ATLS_CHACHA_SOP
+#define ATLS_CHACHA_SOP 1
+#endif
 #ifndef ATLS_CHACHA_OPEN_MAC_FIRST
 #define ATLS_CHACHA_OPEN_MAC_FIRST 2
 #endif
 typedef uint32_t v4u32_ch __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4u32_ch lds_uint4;
-template <bool OPEN, int G, bool LATE, bool CARRY = false>
+template <bool OPEN, int G, bool LATE, bool CARRY = false, bool PRE = G == 64>
 __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl,
                               lds_uint4* lds = nullptr) {
   // TLS and WIRE: nonce from (static IV, seq), 5-byte AAD; WIRE also frames the record
@@ -220,6 +261,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   P130 acc = p_zero(), innerL = p_zero();
   int64_t lastnz = -1;
   constexpr bool MAC_FIRST = OPEN && G != 64 && (CARRY ? ATLS_CHACHA_OPEN_MAC_FIRST >= 2 : ATLS_CHACHA_OPEN_MAC_FIRST >= 1);
+  constexpr bool SOP = ATLS_CHACHA_SOP && !OPEN && !LATE;  // full seal slots: one reduction (p_sop4)
   const uint32_t mis = CARRY ? (uint32_t)((reinterpret_cast<uintptr_t>(dst) - 64u) & 127u) : 0u;
   uint32_t cmask = 0, coff = 0;  // CARRY: pieces of the block at record offset coff waiting in LDS
   auto flush = [&]() {
@@ -241,7 +283,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     // its keystream is computed, so the load's latency (PCIe when the kernel reads pinned host
     // memory) hides under the ChaCha rounds. The throughput paths keep the registers free instead.
     uint4 pre[4] = {};
-    if (G == 64 && active && j >= 1 && j <= jmax && 64u * (j - 1) + 64u <= len) {
+    if (PRE && active && j >= 1 && j <= jmax && 64u * (j - 1) + 64u <= len) {
 #pragma unroll
       for (int q = 0; q < 4; q++) pre[q] = ld16(src + 64u * (j - 1) + 16 * q);
     }
@@ -274,6 +316,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 
     P130 inner = p_zero();
     uint32_t cnt = 0;
+    bool sop = false;
     if (j == 0) {  // AAD blocks (get_mac_data: aad || pad16, poly1305.rs:57-59)
       for (uint32_t i = 0; i < na; i++) {
         uint32_t B[4] = {0, 0, 0, 0};
@@ -322,7 +365,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         if (off + 64 <= len) {
 #pragma unroll
           for (int q = 0; q < 4; q++) {
-            const uint4 v = G == 64 ? pre[q] : ld16(src + off + 16 * q);
+            const uint4 v = PRE ? pre[q] : ld16(src + off + 16 * q);
             P[4 * q] = v.x; P[4 * q + 1] = v.y; P[4 * q + 2] = v.z; P[4 * q + 3] = v.w;
           }
         } else {
@@ -380,6 +423,9 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
               }
             }
           }
+        } else if (SOP && valid == 64u) {
+          p_sop4(acc, base == 0, r64, P, r, rsq, rcu);  // seal: the MAC over the ciphertext just written
+          sop = true;
         } else {
           fold(P);  // seal: the MAC runs over the ciphertext just written
         }
@@ -390,7 +436,9 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         fold(Z);
       }
     }
-    if (j == jL) {
+    if (sop) {
+      // acc already holds this slot (p_sop4)
+    } else if (j == jL) {
       innerL = inner;  // ref = Q-1: contributes inner * r^1
     } else {
       if (base) acc = p_mul(acc, r64);  // r^(4G) = r^64; a lane's first slot is in the first step
@@ -481,7 +529,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 
 // One group of G lanes seals / opens the record at work-list position q (direct batches: the
 // kernel validates the descriptor itself).
-template <bool OPEN, int G, bool LATE, bool CARRY = false>
+template <bool OPEN, int G, bool LATE, bool CARRY = false, bool PRE = G == 64>
 __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W, uint32_t q, uint32_t cnt, int gl,
                                              lds_uint4* lds = nullptr) {
   if (q >= cnt) return;
@@ -497,7 +545,7 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
       }
     }
   } else {
-    chacha_record<OPEN, G, LATE, CARRY>(A, d, A.ks + d.key_slot, r, gl, lds);
+    chacha_record<OPEN, G, LATE, CARRY, PRE>(A, d, A.ks + d.key_slot, r, gl, lds);
   }
 }
 
@@ -570,7 +618,7 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
 #endif
 
 // Direct batch: P positions per wave and step, the width chosen per step from their longest record.
-template <bool OPEN>
+template <bool OPEN, bool PRE = false>
 __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
   __shared__ v4u32_ch carry[256 * 4];  // CARRY: 4 pieces of 16 B per lane (16 KiB per workgroup)
   lds_uint4* lds = (lds_uint4*)(carry) + 4u * threadIdx.x;
@@ -587,13 +635,13 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
     mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
     if (ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY) {
       constexpr int G = ATLS_CHACHA_TINY ? ATLS_CHACHA_TINY_G : 4;
-      chacha_group<OPEN, G, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
+      chacha_group<OPEN, G, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
     } else if (mx <= (uint32_t)ATLS_CHACHA_SHORT) {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3, lds);
+      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3, lds);
     } else {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15, lds);
+      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15, lds);
     }
   }
 }
@@ -603,6 +651,23 @@ __global__ __launch_bounds__(256, PLANNED ? (OPEN ? ATLS_CHACHA_MINW_SIDE_OPEN :
   const int lane = threadIdx.x & 63;
   if constexpr (PLANNED) chacha_batch<OPEN, ATLS_CHACHA_PLANNED_G>(A, lane);
   else chacha_direct<OPEN>(A, lane);
+}
+
+// Direct opens that give at most two waves per SIMD (C3: 65,536 MTU-sized records = 2,048 waves of 32
+// records on 1,024 SIMDs) lose nothing to a 2-wave register bound, and 256 VGPRs let each lane load its
+// slot's data before computing the keystream (PRE) without spilling. The C3 kernels' waves sat at
+// s_waitcnt a quarter of their cycles (profiles/r03/c3_pmc_stall_*.csv). Same-box A/B over 3 rounds
+// (profiles/r03/ab_c3_w2.log): C3 open 0.1016 -> 0.1003 ms (0.1005 without PRE); C3 seal 0.0878 ->
+// 0.0908 ms with PRE, 0.0874 without, so seals keep the 3-wave kernel (where SOP took them to 0.0840).
+#ifndef ATLS_CHACHA_W2
+#define ATLS_CHACHA_W2 1
+#endif
+#ifndef ATLS_CHACHA_W2_PRE
+#define ATLS_CHACHA_W2_PRE 1
+#endif
+template <bool OPEN>
+__global__ __launch_bounds__(256, 2) void chacha_kernel_w2(ChArgs A) {  // OPEN only (launch below)
+  chacha_direct<OPEN, (bool)ATLS_CHACHA_W2_PRE>(A, threadIdx.x & 63);
 }
 
 // Latency path for a few records (the Cipher-trait single call, record.rs:191-193): one record per
@@ -628,7 +693,8 @@ __global__ __launch_bounds__(64) void chacha_kernel_lat(ChArgs A) {
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
-                                  uint32_t n_slots, int grid, hipStream_t s, uint32_t* done, uint32_t done_val) {
+                                  uint32_t n_slots, int grid, hipStream_t s, uint32_t* done, uint32_t done_val,
+                                  int cus) {
   if (n == 0) return 0;
   atls::ChArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, idx,
                  (atls::PlanHdr*)plan, err, n_slots, n == 1 ? done : nullptr, done_val};
@@ -642,6 +708,9 @@ extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs
   } else if (idx) {
     if (open) hipLaunchKernelGGL((atls::chacha_kernel<true, true>), dim3(g), dim3(256), 0, s, A);
     else hipLaunchKernelGGL((atls::chacha_kernel<false, true>), dim3(g), dim3(256), 0, s, A);
+  } else if (ATLS_CHACHA_W2 && open && cus > 0 && (n + 31u) / 32u <= 8u * (uint32_t)cus) {
+    // a wave step covers 32 positions: at most 2 waves per SIMD of work (chacha_kernel_w2)
+    hipLaunchKernelGGL((atls::chacha_kernel_w2<true>), dim3(g), dim3(256), 0, s, A);
   } else {
     if (open) hipLaunchKernelGGL((atls::chacha_kernel<true, false>), dim3(g), dim3(256), 0, s, A);
     else hipLaunchKernelGGL((atls::chacha_kernel<false, false>), dim3(g), dim3(256), 0, s, A);

@@ -43,7 +43,8 @@ extern "C" int atls_launch_group(const atls_rec* recs, uint32_t n, uint32_t n_sl
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
                                   const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                   atls_open_result* res, const uint32_t* idx, void* plan, uint32_t* err,
-                                  uint32_t n_slots, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
+                                  uint32_t n_slots, int grid, hipStream_t s, uint32_t* done, uint32_t done_val,
+                                  int cus);
 extern "C" int atls_launch_hash(int op, uint32_t hl, const uint8_t* data, const atls_span* keys, const atls_span* msgs,
                                 uint32_t n, uint32_t out_len, uint8_t* out, hipStream_t s);
 extern "C" int atls_launch_key_schedule(uint32_t hl, const uint8_t* shared, uint32_t shared_len, const uint8_t* hello,
@@ -97,8 +98,14 @@ struct atls_engine {
   DevBuf grp_cnt, grp_aux, grp_idx;          // key groups of direct AES-GCM batches (plan.hip)
   uint32_t group_min = 2048;                 // ATLS_GCM_GROUP_MIN: smallest batch to group (0: never)
   int chacha_wgs = 8;                        // ATLS_CHACHA_WGS: ChaCha20-Poly1305 workgroups per CU
+  bool chacha_w2 = true;                     // ATLS_CHACHA_W2=0: direct batches never take the 2-wave kernel
   bool force_plan = false;                   // ATLS_FORCE_PLAN=1: plan every batch (tests)
   bool no_pipeline = false;                  // ATLS_NO_PIPELINE=1: stage host batches in one piece
+  // Host-memory batches (run_host_pipelined): an upload and a download stream beside the engine stream,
+  // created on the first such batch, and two events per chunk.
+  hipStream_t up = nullptr, down = nullptr;
+  std::vector<hipEvent_t> pev;
+  bool zero_copy = false;                    // ATLS_ZERO_COPY=1: kernels read / write pinned host buffers in place
   std::mutex mu;
 };
 
@@ -146,6 +153,25 @@ size_t rec_out_len(const atls_rec& r, bool open) {
 }
 
 // Largest byte extent touched by the descriptors (host-memory mode only).
+// The device address of a page-locked, device-mapped host range [p, p + len) (hipHostMalloc /
+// hipHostRegister memory, e.g. torch pin_memory), or nullptr for pageable memory.
+void* host_alias(const void* p, size_t len) {
+  if (!p || !len) return nullptr;
+  hipPointerAttribute_t a, b;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer) return nullptr;
+  const uint8_t* last = (const uint8_t*)p + len - 1;
+  if (hipPointerGetAttributes(&b, last) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (b.type != hipMemoryTypeHost || (uint8_t*)b.devicePointer != (uint8_t*)a.devicePointer + (len - 1)) return nullptr;
+  return a.devicePointer;
+}
+
 void extents(const atls_rec* recs, uint32_t n, bool open, size_t* in_end, size_t* out_end, size_t* aux_end) {
   size_t a = 0, b = 0, c = 0;
   for (uint32_t i = 0; i < n; i++) {
@@ -165,20 +191,26 @@ int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n
   // direct batches only (one record kernel in the key table)
   if (e->has_chacha)
     return atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, nullptr,
-                              nullptr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s, done, done_val);
+                              nullptr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s, done, done_val,
+                              e->chacha_w2 ? e->cus : 0);
   return atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, nullptr, nullptr, (uint32_t*)e->err.p, e->n_slots,
                          e->aes_nr_mask, nullptr, nullptr, e->cus, s, done, done_val);
 }
 
-// Host-memory batch (the socket path) in record chunks of ~kChunkBytes, alternating between the
-// engine's two streams: chunk c+1's host-to-device copy overlaps chunk c's kernel and its
-// device-to-host copy (separate DMA engines; full speed with pinned host buffers). Needs records
-// whose input and output ranges increase with the record index. When every record has the same
-// output length and the outputs sit at a fixed pitch, only record bytes travel back
-// (hipMemcpy2DAsync), so the bytes of `out` between records need not be staged in: they stay as
-// the caller had them. Otherwise each chunk's whole output range is staged in and copied back.
-// Returns -1 when the batch does not qualify (the caller then stages the batch in one piece).
+// Host-memory batch in record-aligned chunks over three streams: every chunk's input goes up on the
+// upload stream, its kernel runs on the engine stream once that copy is done, and its output comes back
+// on the download stream once the kernel is done. Each direction of the link then has one stream that is
+// never idle while chunks remain, so uploads of later chunks run beside downloads of earlier ones the
+// whole time. tools/ubench/pcie_probe.hip (profiles/r03/pcie_probe.log): PCIe Gen5 gives 57 GB/s one way
+// and 48.5 GB/s per direction both ways at once; chunked copies on the round-2 scheme (chunk k's upload,
+// kernel and download on one of two streams in turn) reach 40.4 without any kernel. Measured C2 from
+// pinned memory: 37.1 GiB/s (round 2 scheme) -> 37.96 (this one, 32 MiB chunks); 16 MiB chunks 32.1,
+// 8 MiB 26.6 -- a fixed cost per chunk, not the link, sets the rate at small chunks.
+// A fixed-pitch output layout (all records the same stride, the C2/C4 case) comes back with
+// hipMemcpy2DAsync, so the bytes between records are never read or written; other layouts stage each
+// chunk's output range in and out. Returns -1 when the records are not in ascending order (the caller
+// stages the batch in one piece).
 int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
                        void* out, uint8_t* tags_out, const uint8_t* tags_in, atls_open_result* res,
                        size_t in_end, size_t out_end, size_t aux_end) {
@@ -192,15 +224,18 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   for (uint32_t i = 1; i < n; i++)
     if (recs[i].in_off < recs[i - 1].in_off + ilen(recs[i - 1]) || recs[i].out_off < recs[i - 1].out_off + olen(recs[i - 1]))
       return -1;
+  if (!e->up && (hipStreamCreateWithFlags(&e->up, hipStreamNonBlocking) != hipSuccess ||
+                 hipStreamCreateWithFlags(&e->down, hipStreamNonBlocking) != hipSuccess))
+    return ATLS_INTERNAL_ERROR;
   bool pitched = n > 1;
   const size_t pitch = n > 1 ? (size_t)(recs[1].out_off - recs[0].out_off) : 0, width = olen(recs[0]);
   for (uint32_t i = 1; i < n && pitched; i++)
     pitched = olen(recs[i]) == width && recs[i].out_off == recs[0].out_off + i * pitch;
-  hipStream_t st[2] = {e->stream, e->stream2};
-  hipEvent_t ev[2] = {e->ev_plan, e->ev_side};
-  // descriptors, aux and err are in place (stream 0) before the other stream starts
-  if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, st[0]) != hipSuccess) return ATLS_INTERNAL_ERROR;
-  if (hipEventRecord(ev[0], st[0]) != hipSuccess || hipStreamWaitEvent(st[1], ev[0], 0) != hipSuccess)
+  hipStream_t ks = e->stream, up = e->up, down = e->down;
+  // the batch's descriptors and aux are in place, and the engine's earlier batches (which used the same
+  // staging buffers) are done, before the first upload
+  if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, ks) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  if (hipEventRecord(e->ev_plan, ks) != hipSuccess || hipStreamWaitEvent(up, e->ev_plan, 0) != hipSuccess)
     return ATLS_INTERNAL_ERROR;
   const auto* d_recs = (const atls_rec*)e->recs.p;
   auto* d_in = (uint8_t*)e->in.p;
@@ -209,43 +244,53 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   auto* d_res = (atls_open_result*)e->res.p;
   (void)in_end;
   (void)out_end;
-  int c = 0;
-  for (uint32_t a = 0; a < n; c ^= 1) {
+  size_t k = 0;
+  for (uint32_t a = 0; a < n; k++) {
     uint32_t b = a + 1;
     while (b < n && recs[b - 1].in_off + ilen(recs[b - 1]) - recs[a].in_off < kChunkBytes) b++;
-    hipStream_t s = st[c];
+    while (e->pev.size() < 2 * (k + 1)) {
+      hipEvent_t ev;
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return ATLS_INTERNAL_ERROR;
+      e->pev.push_back(ev);
+    }
+    hipEvent_t uploaded = e->pev[2 * k], sealed = e->pev[2 * k + 1];
     const size_t in_lo = recs[a].in_off, in_hi = recs[b - 1].in_off + ilen(recs[b - 1]);
     const size_t out_lo = recs[a].out_off, out_hi = recs[b - 1].out_off + olen(recs[b - 1]);
     const uint32_t cnt = b - a;
     if (in_hi > in_lo &&
-        hipMemcpyAsync(d_in + in_lo, (const uint8_t*)in + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, s) != hipSuccess)
+        hipMemcpyAsync(d_in + in_lo, (const uint8_t*)in + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, up) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     if (open && tags_in && hipMemcpyAsync(d_tags + 16 * (size_t)a, tags_in + 16 * (size_t)a, 16 * (size_t)cnt,
-                               hipMemcpyHostToDevice, s) != hipSuccess)
+                               hipMemcpyHostToDevice, up) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     if (!pitched && out_hi > out_lo &&
-        hipMemcpyAsync(d_out + out_lo, (uint8_t*)out + out_lo, out_hi - out_lo, hipMemcpyHostToDevice, s) != hipSuccess)
+        hipMemcpyAsync(d_out + out_lo, (uint8_t*)out + out_lo, out_hi - out_lo, hipMemcpyHostToDevice, up) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+    if (hipEventRecord(uploaded, up) != hipSuccess || hipStreamWaitEvent(ks, uploaded, 0) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     int rc = launch_records(e, open, d_recs + a, cnt, d_in, (const uint8_t*)e->aux.p, d_out, d_tags + 16 * (size_t)a,
-                            d_tags + 16 * (size_t)a, d_res + a, s);
+                            d_tags + 16 * (size_t)a, d_res + a, ks);
     if (rc) return rc;
+    if (hipEventRecord(sealed, ks) != hipSuccess || hipStreamWaitEvent(down, sealed, 0) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
     if (pitched) {
       if (width && hipMemcpy2DAsync((uint8_t*)out + out_lo, pitch, d_out + out_lo, pitch, width, cnt,
-                                    hipMemcpyDeviceToHost, s) != hipSuccess)
+                                    hipMemcpyDeviceToHost, down) != hipSuccess)
         return ATLS_INTERNAL_ERROR;
     } else if (out_hi > out_lo &&
-               hipMemcpyAsync((uint8_t*)out + out_lo, d_out + out_lo, out_hi - out_lo, hipMemcpyDeviceToHost, s) != hipSuccess) {
+               hipMemcpyAsync((uint8_t*)out + out_lo, d_out + out_lo, out_hi - out_lo, hipMemcpyDeviceToHost, down) != hipSuccess) {
       return ATLS_INTERNAL_ERROR;
     }
     if (!open && tags_out && hipMemcpyAsync(tags_out + 16 * (size_t)a, d_tags + 16 * (size_t)a, 16 * (size_t)cnt,
-                                hipMemcpyDeviceToHost, s) != hipSuccess)
+                                hipMemcpyDeviceToHost, down) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
-    if (open && hipMemcpyAsync(res + a, d_res + a, sizeof(atls_open_result) * (size_t)cnt, hipMemcpyDeviceToHost, s) !=
+    if (open && hipMemcpyAsync(res + a, d_res + a, sizeof(atls_open_result) * (size_t)cnt, hipMemcpyDeviceToHost, down) !=
                     hipSuccess)
       return ATLS_INTERNAL_ERROR;
     a = b;
   }
-  if (hipEventRecord(ev[1], st[1]) != hipSuccess || hipStreamWaitEvent(st[0], ev[1], 0) != hipSuccess)
+  // the engine stream is ordered after the last download (finish synchronises it)
+  if (hipEventRecord(e->ev_side, down) != hipSuccess || hipStreamWaitEvent(ks, e->ev_side, 0) != hipSuccess)
     return ATLS_INTERNAL_ERROR;
   return finish(e, 0);
 }
@@ -291,8 +336,32 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   // small launches that sort records into per-kernel lists, longest first.
   const int kinds = (e->has_chacha ? 1 : 0) + __builtin_popcount((unsigned)e->aes_nr_mask);
   const bool planned = kinds > 1 || e->force_plan;
+  bool zc = false;
   if (!dev_ptrs) {
     extents(recs, n, open, &in_end, &out_end, &aux_end);
+    // Zero copy (opt-in): every host buffer of the batch is page-locked and mapped, so the kernels read
+    // the records from host memory and write their output there in place, over PCIe, with no staging
+    // copies. C2 from pinned memory 34.5 GiB/s against 32.1 staged at 16 MiB chunks and 37.96 at 32 MiB
+    // (profiles/r03/bench_c2_pcie_*.log): the lane groups' 128-B runs of 8 records 16 KiB apart touch
+    // many host pages at once, where a copy engine streams.
+    if (e->zero_copy) {
+      const void* zi = in_end ? host_alias(in, in_end) : e->in.p;
+      void* zo = out_end ? host_alias(out, out_end) : e->out.p;
+      const void* za = aux_end ? host_alias(aux, aux_end) : e->aux.p;
+      const void* zt = no_tags ? e->tags.p : host_alias(open ? (const void*)tags_in : (const void*)tags_out, 16 * (size_t)n);
+      void* zr = open ? host_alias(res, sizeof(atls_open_result) * (size_t)n) : (void*)res;
+      if (zi && zo && za && zt && (zr || !open)) {
+        zc = true;
+        d_in = (const uint8_t*)zi;
+        d_out = (uint8_t*)zo;
+        d_aux = (const uint8_t*)za;
+        d_tags_out = (uint8_t*)zt;
+        d_tags_in = (const uint8_t*)zt;
+        d_res = (atls_open_result*)zr;
+      }
+    }
+  }
+  if (!dev_ptrs && !zc) {
     if (!e->in.reserve(in_end + 16) || !e->out.reserve(out_end + 16) || !e->aux.reserve(aux_end + 16) ||
         !e->tags.reserve(16 * (size_t)n) || !e->res.reserve(sizeof(atls_open_result) * (size_t)n))
       return ATLS_INTERNAL_ERROR;
@@ -352,7 +421,8 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
       cs = e->stream2;
     }
     rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, idx,
-                            plan_hdr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs, nullptr, 0);
+                            plan_hdr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs, nullptr, 0,
+                            e->chacha_w2 ? e->cus : 0);
     if (rc) return rc;
     if (side && hipEventRecord(ps.side_done, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
@@ -385,6 +455,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     if (lazy) ps.pending = true;
     else if (hipStreamWaitEvent(s, ps.side_done, 0) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
+  if (zc) return finish(e, flags & ~ATLS_FLAG_NO_SYNC);  // host buffers: the batch ends before the call returns
   if (!dev_ptrs) {
     if (out_end && hipMemcpyAsync(out, e->out.p, out_end, hipMemcpyDeviceToHost, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
@@ -751,6 +822,8 @@ atls_engine* atls_engine_create(int device) {
   if (const char* v = std::getenv("ATLS_FORCE_PLAN")) e->force_plan = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_NO_PIPELINE")) e->no_pipeline = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_CHACHA_WGS")) e->chacha_wgs = std::max(1, std::atoi(v));
+  if (const char* v = std::getenv("ATLS_CHACHA_W2")) e->chacha_w2 = std::atoi(v) != 0;
+  if (const char* v = std::getenv("ATLS_ZERO_COPY")) e->zero_copy = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_GCM_GROUP_MIN")) e->group_min = (uint32_t)std::max(0, std::atoi(v));
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || hipMemsetAsync(e->err.p, 0, 16, e->stream) != hipSuccess ||
       atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
@@ -775,6 +848,9 @@ void atls_engine_destroy(atls_engine* e) {
   }
   if (e->ev_plan) (void)hipEventDestroy(e->ev_plan);
   if (e->ev_side) (void)hipEventDestroy(e->ev_side);
+  for (hipEvent_t ev : e->pev) (void)hipEventDestroy(ev);
+  if (e->up) (void)hipStreamDestroy(e->up);
+  if (e->down) (void)hipStreamDestroy(e->down);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;

@@ -1,8 +1,10 @@
-"""GPU: host-memory batches through the engine's chunked two-stream pipeline (engine.cpp
-run_host_pipelined): several 32 MiB chunks, the fixed-pitch layout (record bytes copied back with
-hipMemcpy2DAsync, bytes between records untouched) and a variable-length layout (each chunk's
-output range staged in and out). Results are checked against the oracle record by record, and
-the bytes of `out` between records must come back as the caller left them."""
+"""GPU: host-memory batches through the engine's chunked pipeline (engine.cpp run_host_pipelined:
+uploads, kernels and downloads on three streams): several chunks, the fixed-pitch layout (record bytes
+copied back with hipMemcpy2DAsync, bytes between records untouched) and a variable-length layout (each
+chunk's output range staged in and out); and the same batches in page-locked host buffers with
+ATLS_ZERO_COPY=1, where the kernels read and write the host buffers in place (engine.cpp host_alias).
+Results are checked against the oracle record by record, and the bytes of `out` between records must
+come back as the caller left them."""
 import numpy as np
 import pytest
 
@@ -20,14 +22,24 @@ def atls():
     return a
 
 
-def _check(atls, b, seed):
+def _host(nbytes, pinned):
+    if not pinned:
+        return np.zeros(nbytes, np.uint8)
+    import torch
+
+    return torch.zeros(nbytes, dtype=torch.uint8, pin_memory=True).numpy()
+
+
+def _check(atls, b, seed, pinned=False):
     eng = atls.Engine(0)
     eng.set_keys(b["keys"])
     rng = np.random.default_rng(seed)
     n = len(b["recs"])
-    inbuf = rng.integers(0, 256, b["in_bytes"] + 16, dtype=np.uint8)
-    out = np.full(b["out_bytes"] + 16, 0xA5, np.uint8)  # gap bytes must survive
-    tags = np.zeros(16 * n, np.uint8)
+    inbuf = _host(b["in_bytes"] + 16, pinned)
+    inbuf[:] = rng.integers(0, 256, b["in_bytes"] + 16, dtype=np.uint8)
+    out = _host(b["out_bytes"] + 16, pinned)
+    out[:] = 0xA5  # gap bytes must survive
+    tags = _host(16 * n, pinned)
     eng.seal_batch(b["recs"], inbuf, np.zeros(16, np.uint8), out, tags)
     okeys = (ora.OraKey * len(b["keys"])).from_buffer_copy(b["keys"].tobytes())
     orecs = (ora.OraRec * n).from_buffer_copy(b["recs"].tobytes())
@@ -39,8 +51,8 @@ def _check(atls, b, seed):
     # and back: open in host memory through the same pipeline
     r2 = b["recs"].copy()
     r2["in_off"], r2["len"] = b["recs"]["out_off"], b["recs"]["len"] + 1
-    pt = np.zeros_like(out)
-    res = np.zeros(n, atls.OPEN_RESULT_DTYPE)
+    pt = _host(out.nbytes, pinned)
+    res = _host(n * atls.OPEN_RESULT_DTYPE.itemsize, pinned).view(atls.OPEN_RESULT_DTYPE)
     eng.open_batch(r2, out, np.zeros(16, np.uint8), tags, pt, res)
     assert (res["status"] == 0).all() and (res["content_len"] == b["recs"]["len"]).all()
     for i in range(0, n, max(1, n // 64)):
@@ -50,16 +62,29 @@ def _check(atls, b, seed):
     eng.close()
 
 
-def test_pitched_layout_multi_chunk(atls):
+@pytest.mark.parametrize("zero_copy", [False, True], ids=["staged", "zero-copy"])
+def test_pitched_layout_multi_chunk(atls, zero_copy, monkeypatch):
     from anothertls_amd import workload
 
-    b = workload.tls_batch(6000, 16000, 0x1301, n_keys=64)  # ~96 MiB: 3 chunks, fixed pitch
-    _check(atls, b, 5)
+    monkeypatch.setenv("ATLS_ZERO_COPY", "1" if zero_copy else "0")
+    b = workload.tls_batch(6000, 16000, 0x1301, n_keys=64)  # ~96 MiB: 6 chunks, fixed pitch
+    _check(atls, b, 5, pinned=zero_copy)
 
 
-def test_variable_layout_multi_chunk(atls):
+@pytest.mark.parametrize("zero_copy", [False, True], ids=["staged", "zero-copy"])
+def test_variable_layout_multi_chunk(atls, zero_copy, monkeypatch):
     from anothertls_amd import workload
 
+    monkeypatch.setenv("ATLS_ZERO_COPY", "1" if zero_copy else "0")
     lens = np.random.default_rng(9).integers(0, 16385, 9000).astype(np.uint64)
     b = workload.tls_batch(len(lens), lens, 0x1303, n_keys=32)  # ~72 MiB, staged chunks
-    _check(atls, b, 6)
+    _check(atls, b, 6, pinned=zero_copy)
+
+
+def test_zero_copy_mixed_suites_planned(atls, monkeypatch):
+    """A planned (AES-GCM + ChaCha20-Poly1305) batch in page-locked buffers, read and written in place."""
+    from anothertls_amd import workload
+
+    monkeypatch.setenv("ATLS_ZERO_COPY", "1")
+    b = workload.shard_batch("c5_mixed_256Ki_x_64B-16KiB", 0, n=3000)
+    _check(atls, b, 7, pinned=True)
