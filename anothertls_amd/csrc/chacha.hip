@@ -261,7 +261,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   P130 acc = p_zero(), innerL = p_zero();
   int64_t lastnz = -1;
   constexpr bool MAC_FIRST = OPEN && G != 64 && (CARRY ? ATLS_CHACHA_OPEN_MAC_FIRST >= 2 : ATLS_CHACHA_OPEN_MAC_FIRST >= 1);
-  constexpr bool SOP = ATLS_CHACHA_SOP && !OPEN && !LATE;  // full seal slots: one reduction (p_sop4)
+  constexpr bool SOP = ATLS_CHACHA_SOP && !LATE;  // full slots: one reduction (p_sop4)
   const uint32_t mis = CARRY ? (uint32_t)((reinterpret_cast<uintptr_t>(dst) - 64u) & 127u) : 0u;
   uint32_t cmask = 0, coff = 0;  // CARRY: pieces of the block at record offset coff waiting in LDS
   auto flush = [&]() {
@@ -384,7 +384,12 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
           // MAC over the received ciphertext first, then the plaintext in the same registers (no
           // second 16-word block live beside the keystream: the open kernels stay within their caps)
           mask_valid(P, valid);
-          fold(P);
+          if (SOP && valid == 64u) {
+            p_sop4(acc, base == 0, r64, P, r, rsq, rcu);
+            sop = true;
+          } else {
+            fold(P);
+          }
           if (MAC_FIRST) chacha_block(kw, j, nw, ks);
 #pragma unroll
           for (int q = 0; q < 16; q++) P[q] = skip_xor ? P[q] : (P[q] ^ ks[q]);
@@ -581,6 +586,10 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 #ifndef ATLS_CHACHA_MINW_SIDE_OPEN
 #define ATLS_CHACHA_MINW_SIDE_OPEN ATLS_CHACHA_MINW_SIDE
 #endif
+#ifndef ATLS_CHACHA_PLANNED_EARLY
+#define ATLS_CHACHA_PLANNED_EARLY 0  // 1: planned seals keep r^2, r^3 live and fold full slots by SOP -- 31
+                                     // spilled VGPRs at the 128 cap, C5 seal 0.327 -> 0.349 ms (ab_c35_early.log)
+#endif
 #ifndef ATLS_CHACHA_PLANNED_G
 #define ATLS_CHACHA_PLANNED_G 16  // lanes per record in planned (mixed) batches; C5 0.341 ms at 16, 0.359 at
                                   // 8, 0.435 at 4 (profiles/r02/ab_chacha_planned_g.log)
@@ -593,7 +602,7 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
   const uint32_t stride = gridDim.x * blockDim.x / 64u * kPer;
   for (uint32_t q0 = wave * kPer; q0 < cnt; q0 += stride)
-    chacha_group<OPEN, G, true>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
+    chacha_group<OPEN, G, OPEN || !ATLS_CHACHA_PLANNED_EARLY>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
 }
 
 // Records up to ATLS_CHACHA_TINY bytes (every record of a wave step) take ATLS_CHACHA_TINY_G
@@ -617,9 +626,21 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
 #define ATLS_CHACHA_CARRY_SEAL 0
 #endif
 
+#ifndef ATLS_CHACHA_W2
+#define ATLS_CHACHA_W2 1
+#endif
+#ifndef ATLS_CHACHA_W2_PRE
+#define ATLS_CHACHA_W2_PRE 1
+#endif
+#ifndef ATLS_CHACHA_W2_EARLY
+#define ATLS_CHACHA_W2_EARLY 1  // the 2-wave kernel keeps r^2, r^3 live (not LATE), so its opens fold by SOP too:
+                                // C3 open 0.1015 -> 0.0977 ms (profiles/r03/ab_c35_early.log)
+#endif
+
 // Direct batch: P positions per wave and step, the width chosen per step from their longest record.
 template <bool OPEN, bool PRE = false>
 __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
+  constexpr bool LATE = OPEN && !(PRE && ATLS_CHACHA_W2_EARLY);
   __shared__ v4u32_ch carry[256 * 4];  // CARRY: 4 pieces of 16 B per lane (16 KiB per workgroup)
   lds_uint4* lds = (lds_uint4*)(carry) + 4u * threadIdx.x;
   const WorkList W{nullptr, nullptr, kListChacha, A.n};
@@ -635,13 +656,13 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
     mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
     if (ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY) {
       constexpr int G = ATLS_CHACHA_TINY ? ATLS_CHACHA_TINY_G : 4;
-      chacha_group<OPEN, G, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
+      chacha_group<OPEN, G, LATE, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
     } else if (mx <= (uint32_t)ATLS_CHACHA_SHORT) {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3, lds);
+      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, LATE, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3, lds);
     } else {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, OPEN, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15, lds);
+      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, LATE, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15, lds);
     }
   }
 }
@@ -659,12 +680,6 @@ __global__ __launch_bounds__(256, PLANNED ? (OPEN ? ATLS_CHACHA_MINW_SIDE_OPEN :
 // s_waitcnt a quarter of their cycles (profiles/r03/c3_pmc_stall_*.csv). Same-box A/B over 3 rounds
 // (profiles/r03/ab_c3_w2.log): C3 open 0.1016 -> 0.1003 ms (0.1005 without PRE); C3 seal 0.0878 ->
 // 0.0908 ms with PRE, 0.0874 without, so seals keep the 3-wave kernel (where SOP took them to 0.0840).
-#ifndef ATLS_CHACHA_W2
-#define ATLS_CHACHA_W2 1
-#endif
-#ifndef ATLS_CHACHA_W2_PRE
-#define ATLS_CHACHA_W2_PRE 1
-#endif
 template <bool OPEN>
 __global__ __launch_bounds__(256, 2) void chacha_kernel_w2(ChArgs A) {  // OPEN only (launch below)
   chacha_direct<OPEN, (bool)ATLS_CHACHA_W2_PRE>(A, threadIdx.x & 63);
