@@ -7,6 +7,8 @@
 //   zc_read / zc_write      a kernel reading host memory into HBM / writing HBM into host memory
 //                           (16-B loads / stores per lane, mapped pinned memory)
 //   zc_both                 both kernels at once on two streams
+//   dma_d2h_2d / dma_h2d_2d C2's record layout (65,536 rows of 16,385 B at a 16,400-B pitch) copied
+//                           with hipMemcpy2DAsync, one call, and in 32 MiB chunks (2,048 rows each)
 // Rates are GB/s per direction (1e9 B/s).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -67,6 +69,13 @@ static void f_chunk(void*) {
     CK(hipMemcpyAsync(C.h_out + o, C.d_out + o, m, hipMemcpyDeviceToHost, s));
   }
 }
+static const size_t kW = 16385, kP = 16400, kRows = 65536;
+static void f_d2h_2d(void*) { CK(hipMemcpy2DAsync(C.h_out, kP, C.d_out, kP, kW, kRows, hipMemcpyDeviceToHost, C.s0)); }
+static void f_h2d_2d(void*) { CK(hipMemcpy2DAsync(C.d_in, kP, C.h_in, kP, kW, kRows, hipMemcpyHostToDevice, C.s0)); }
+static void f_d2h_2d_chunk(void*) {
+  for (size_t r = 0; r < kRows; r += 2048)
+    CK(hipMemcpy2DAsync(C.h_out + r * kP, kP, C.d_out + r * kP, kP, kW, 2048, hipMemcpyDeviceToHost, C.s0));
+}
 static void f_zc_read(void*) {
   hipLaunchKernelGGL(copy16, dim3(C.grid), dim3(256), 0, C.s0, (const uint4*)C.hd_in, (uint4*)C.d_in, C.n / 16);
 }
@@ -80,10 +89,12 @@ static void f_zc_both(void*) {
 
 int main() {
   C.n = (size_t)1 << 30;
-  CK(hipHostMalloc(&C.h_in, C.n, hipHostMallocMapped));
-  CK(hipHostMalloc(&C.h_out, C.n, hipHostMallocMapped));
-  CK(hipMalloc(&C.d_in, C.n));
-  CK(hipMalloc(&C.d_out, C.n));
+  const size_t alloc = C.n + (16u << 20);  // the 2-D layout spans 65,536 x 16,400 B > 1 GiB
+  static_assert(16400ull * 65536ull <= (1ull << 30) + (16ull << 20), "2-D layout fits the buffers");
+  CK(hipHostMalloc(&C.h_in, alloc, hipHostMallocMapped));
+  CK(hipHostMalloc(&C.h_out, alloc, hipHostMallocMapped));
+  CK(hipMalloc(&C.d_in, alloc));
+  CK(hipMalloc(&C.d_out, alloc));
   CK(hipHostGetDevicePointer((void**)&C.hd_in, C.h_in, 0));
   CK(hipHostGetDevicePointer((void**)&C.hd_out, C.h_out, 0));
   for (size_t i = 0; i < C.n; i += 4096) C.h_in[i] = (uint8_t)i;
@@ -102,6 +113,14 @@ int main() {
       for (int r = 0; r < 3; r++) { const float ms = timed(C.s0, C.s1, t.fn, nullptr); best = ms < best ? ms : best; }
       printf("%-12s grid=%-5d %8.3f ms  %6.1f GB/s per direction\n", t.name, grid, best, C.n / (best * 1e6));
     }
+  }
+  struct { const char* name; void (*fn)(void*); } T2[] = {
+      {"dma_d2h_2d", f_d2h_2d}, {"dma_h2d_2d", f_h2d_2d}, {"dma_d2h_2dchunk", f_d2h_2d_chunk}};
+  for (auto& t : T2) {
+    timed(C.s0, C.s1, t.fn, nullptr);
+    float best = 1e9f;
+    for (int r = 0; r < 3; r++) { const float ms = timed(C.s0, C.s1, t.fn, nullptr); best = ms < best ? ms : best; }
+    printf("%-16s %8.3f ms  %6.1f GB/s (record bytes)\n", t.name, best, kW * kRows / (best * 1e6));
   }
   for (size_t mb : {8, 16, 64, 128}) {
     g_chunk = mb << 20;
