@@ -622,6 +622,8 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
 // CARRY on seals: C3 seal traffic 1.28x -> 1.11x of the algorithmic bytes but the kernel 0.0873 ->
 // 0.0905 ms (+3.7 %; 2 more spilled VGPRs); opens 0.1023 -> 0.1004 ms with traffic 1.47x -> 1.29x
 // (profiles/r03/ab_chacha_carry.log). The seal kernel is not HBM-bound, so carry stays on opens only.
+// Re-measured on the SOP seal kernel (profiles/r03/ab_c3_carry_seal_sop.log): traffic 1.31x -> 1.16x,
+// kernel 0.0851 -> 0.0892 ms (+4.8 %); still off.
 #ifndef ATLS_CHACHA_CARRY_SEAL
 #define ATLS_CHACHA_CARRY_SEAL 0
 #endif
