@@ -105,7 +105,7 @@ struct atls_engine {
   // created on the first such batch, and two events per chunk.
   hipStream_t up = nullptr, down = nullptr;
   std::vector<hipEvent_t> pev;
-  bool zero_copy = false;                    // ATLS_ZERO_COPY=1: kernels read / write pinned host buffers in place
+  int zero_copy = 0;  // ATLS_ZERO_COPY: 1 = kernels read and write pinned host buffers in place, 2 = write only
   std::mutex mu;
 };
 
@@ -232,6 +232,20 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   for (uint32_t i = 1; i < n && pitched; i++)
     pitched = olen(recs[i]) == width && recs[i].out_off == recs[0].out_off + i * pitch;
   hipStream_t ks = e->stream, up = e->up, down = e->down;
+  // ATLS_ZERO_COPY=2: the kernels write their output (records, tags, open results) straight into the
+  // page-locked host buffers, so nothing comes back through the download stream and nothing of `out`
+  // is staged in (only record bytes are written); the inputs still go up in chunks.
+  uint8_t* z_out = nullptr;
+  uint8_t* z_tags = nullptr;
+  atls_open_result* z_res = nullptr;
+  if (e->zero_copy == 2 && out_end) {
+    z_out = (uint8_t*)host_alias(out, out_end);
+    const uint8_t* tp = open ? nullptr : tags_out;
+    z_tags = tp ? (uint8_t*)host_alias(tp, 16 * (size_t)n) : nullptr;
+    z_res = open ? (atls_open_result*)host_alias(res, sizeof(atls_open_result) * (size_t)n) : nullptr;
+    if (!z_out || (tp && !z_tags) || (open && !z_res)) z_out = z_tags = nullptr, z_res = nullptr;
+  }
+  const bool zo = z_out != nullptr;
   // the batch's descriptors and aux are in place, and the engine's earlier batches (which used the same
   // staging buffers) are done, before the first upload
   if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, ks) != hipSuccess) return ATLS_INTERNAL_ERROR;
@@ -263,14 +277,19 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
     if (open && tags_in && hipMemcpyAsync(d_tags + 16 * (size_t)a, tags_in + 16 * (size_t)a, 16 * (size_t)cnt,
                                hipMemcpyHostToDevice, up) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
-    if (!pitched && out_hi > out_lo &&
+    if (!zo && !pitched && out_hi > out_lo &&
         hipMemcpyAsync(d_out + out_lo, (uint8_t*)out + out_lo, out_hi - out_lo, hipMemcpyHostToDevice, up) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     if (hipEventRecord(uploaded, up) != hipSuccess || hipStreamWaitEvent(ks, uploaded, 0) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
-    int rc = launch_records(e, open, d_recs + a, cnt, d_in, (const uint8_t*)e->aux.p, d_out, d_tags + 16 * (size_t)a,
-                            d_tags + 16 * (size_t)a, d_res + a, ks);
+    uint8_t* k_tags_out = d_tags + 16 * (size_t)a;
+    if (zo && !open) k_tags_out = z_tags ? z_tags + 16 * (size_t)a : k_tags_out;
+    int rc = launch_records(e, open, d_recs + a, cnt, d_in, (const uint8_t*)e->aux.p, zo ? z_out : d_out, k_tags_out,
+                            d_tags + 16 * (size_t)a, zo && open ? z_res + a : d_res + a, ks);
     if (rc) return rc;
+    const uint32_t a0 = a;
+    a = b;
+    if (zo) continue;  // written in place
     if (hipEventRecord(sealed, ks) != hipSuccess || hipStreamWaitEvent(down, sealed, 0) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
     if (pitched) {
@@ -281,16 +300,15 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
                hipMemcpyAsync((uint8_t*)out + out_lo, d_out + out_lo, out_hi - out_lo, hipMemcpyDeviceToHost, down) != hipSuccess) {
       return ATLS_INTERNAL_ERROR;
     }
-    if (!open && tags_out && hipMemcpyAsync(tags_out + 16 * (size_t)a, d_tags + 16 * (size_t)a, 16 * (size_t)cnt,
+    if (!open && tags_out && hipMemcpyAsync(tags_out + 16 * (size_t)a0, d_tags + 16 * (size_t)a0, 16 * (size_t)cnt,
                                 hipMemcpyDeviceToHost, down) != hipSuccess)
       return ATLS_INTERNAL_ERROR;
-    if (open && hipMemcpyAsync(res + a, d_res + a, sizeof(atls_open_result) * (size_t)cnt, hipMemcpyDeviceToHost, down) !=
+    if (open && hipMemcpyAsync(res + a0, d_res + a0, sizeof(atls_open_result) * (size_t)cnt, hipMemcpyDeviceToHost, down) !=
                     hipSuccess)
       return ATLS_INTERNAL_ERROR;
-    a = b;
   }
   // the engine stream is ordered after the last download (finish synchronises it)
-  if (hipEventRecord(e->ev_side, down) != hipSuccess || hipStreamWaitEvent(ks, e->ev_side, 0) != hipSuccess)
+  if (!zo && (hipEventRecord(e->ev_side, down) != hipSuccess || hipStreamWaitEvent(ks, e->ev_side, 0) != hipSuccess))
     return ATLS_INTERNAL_ERROR;
   return finish(e, 0);
 }
@@ -339,12 +357,13 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   bool zc = false;
   if (!dev_ptrs) {
     extents(recs, n, open, &in_end, &out_end, &aux_end);
-    // Zero copy (opt-in): every host buffer of the batch is page-locked and mapped, so the kernels read
-    // the records from host memory and write their output there in place, over PCIe, with no staging
-    // copies. C2 from pinned memory 34.5 GiB/s against 32.1 staged at 16 MiB chunks and 37.96 at 32 MiB
-    // (profiles/r03/bench_c2_pcie_*.log): the lane groups' 128-B runs of 8 records 16 KiB apart touch
-    // many host pages at once, where a copy engine streams.
-    if (e->zero_copy) {
+    // Zero copy (opt-in, ATLS_ZERO_COPY=1): every host buffer of the batch is page-locked and mapped, so
+    // the kernels read the records from host memory and write their output there in place, over PCIe,
+    // with no staging copies. C2 from pinned memory, same box (profiles/r03/bench_c2_pcie_modes_*.log):
+    // staged 38.2 GiB/s, zero copy 33.9, output-only zero copy (=2, run_host_pipelined) 38.6: the lane
+    // groups' 128-B runs of 8 records 16 KiB apart touch many host pages at once, where a copy engine
+    // streams.
+    if (e->zero_copy == 1) {
       const void* zi = in_end ? host_alias(in, in_end) : e->in.p;
       void* zo = out_end ? host_alias(out, out_end) : e->out.p;
       const void* za = aux_end ? host_alias(aux, aux_end) : e->aux.p;
@@ -823,7 +842,7 @@ atls_engine* atls_engine_create(int device) {
   if (const char* v = std::getenv("ATLS_NO_PIPELINE")) e->no_pipeline = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_CHACHA_WGS")) e->chacha_wgs = std::max(1, std::atoi(v));
   if (const char* v = std::getenv("ATLS_CHACHA_W2")) e->chacha_w2 = std::atoi(v) != 0;
-  if (const char* v = std::getenv("ATLS_ZERO_COPY")) e->zero_copy = std::atoi(v) != 0;
+  if (const char* v = std::getenv("ATLS_ZERO_COPY")) e->zero_copy = std::atoi(v);
   if (const char* v = std::getenv("ATLS_GCM_GROUP_MIN")) e->group_min = (uint32_t)std::max(0, std::atoi(v));
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || hipMemsetAsync(e->err.p, 0, 16, e->stream) != hipSuccess ||
       atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||

@@ -439,19 +439,21 @@ def main():
             for _ in range(3):
                 eng.seal_batch(recs, h_in, np.zeros(16, np.uint8), h_out, h_tags)
             result["pcie_inclusive_GiBps"] = round(3 * payload / (time.perf_counter() - t0) / 2**30, 3)
-            # the same pinned buffers read and written in place by the kernels (ATLS_ZERO_COPY)
-            os.environ["ATLS_ZERO_COPY"] = "1"
-            zeng = atls.Engine(local)
-            del os.environ["ATLS_ZERO_COPY"]
-            zeng.set_keys(batch["keys"])
-            z_out = pinned(batch["out_bytes"])
-            zeng.seal_batch(recs, h_in, np.zeros(16, np.uint8), z_out, h_tags)
-            t0 = time.perf_counter()
-            for _ in range(3):
-                zeng.seal_batch(recs, h_in, np.zeros(16, np.uint8), z_out, h_tags)
-            result["pcie_zero_copy_GiBps"] = round(3 * payload / (time.perf_counter() - t0) / 2**30, 3)
-            result["pcie_zero_copy_equal"] = bool(np.array_equal(z_out, h_out))
-            zeng.close()
+            # the same pinned buffers read and written in place by the kernels (ATLS_ZERO_COPY=1), or
+            # inputs staged in chunks and outputs written in place (=2)
+            for mode, key in ((1, "pcie_zero_copy"), (2, "pcie_zero_copy_out")):
+                os.environ["ATLS_ZERO_COPY"] = str(mode)
+                zeng = atls.Engine(local)
+                del os.environ["ATLS_ZERO_COPY"]
+                zeng.set_keys(batch["keys"])
+                z_out, z_tags = pinned(batch["out_bytes"]), pinned(16 * n)
+                zeng.seal_batch(recs, h_in, np.zeros(16, np.uint8), z_out, z_tags)
+                t0 = time.perf_counter()
+                for _ in range(3):
+                    zeng.seal_batch(recs, h_in, np.zeros(16, np.uint8), z_out, z_tags)
+                result[key + "_GiBps"] = round(3 * payload / (time.perf_counter() - t0) / 2**30, 3)
+                result[key + "_equal"] = bool(np.array_equal(z_out, h_out) and np.array_equal(z_tags, h_tags))
+                zeng.close()
     if args.wire and world == 1 and rank == 0:
         # record framing on the device: header || ct || tag back to back
         wb = workload.wire_batch(batch)

@@ -2,7 +2,8 @@
 uploads, kernels and downloads on three streams): several chunks, the fixed-pitch layout (record bytes
 copied back with hipMemcpy2DAsync, bytes between records untouched) and a variable-length layout (each
 chunk's output range staged in and out); and the same batches in page-locked host buffers with
-ATLS_ZERO_COPY=1, where the kernels read and write the host buffers in place (engine.cpp host_alias).
+ATLS_ZERO_COPY=1, where the kernels read and write the host buffers in place (engine.cpp host_alias),
+and =2, where the inputs go up in chunks and the kernels write their output in place.
 Results are checked against the oracle record by record, and the bytes of `out` between records must
 come back as the caller left them."""
 import numpy as np
@@ -62,23 +63,23 @@ def _check(atls, b, seed, pinned=False):
     eng.close()
 
 
-@pytest.mark.parametrize("zero_copy", [False, True], ids=["staged", "zero-copy"])
+@pytest.mark.parametrize("zero_copy", [0, 1, 2], ids=["staged", "zero-copy", "zero-copy-out"])
 def test_pitched_layout_multi_chunk(atls, zero_copy, monkeypatch):
     from anothertls_amd import workload
 
-    monkeypatch.setenv("ATLS_ZERO_COPY", "1" if zero_copy else "0")
+    monkeypatch.setenv("ATLS_ZERO_COPY", str(zero_copy))
     b = workload.tls_batch(6000, 16000, 0x1301, n_keys=64)  # ~96 MiB: 6 chunks, fixed pitch
-    _check(atls, b, 5, pinned=zero_copy)
+    _check(atls, b, 5, pinned=bool(zero_copy))
 
 
-@pytest.mark.parametrize("zero_copy", [False, True], ids=["staged", "zero-copy"])
+@pytest.mark.parametrize("zero_copy", [0, 1, 2], ids=["staged", "zero-copy", "zero-copy-out"])
 def test_variable_layout_multi_chunk(atls, zero_copy, monkeypatch):
     from anothertls_amd import workload
 
-    monkeypatch.setenv("ATLS_ZERO_COPY", "1" if zero_copy else "0")
+    monkeypatch.setenv("ATLS_ZERO_COPY", str(zero_copy))
     lens = np.random.default_rng(9).integers(0, 16385, 9000).astype(np.uint64)
     b = workload.tls_batch(len(lens), lens, 0x1303, n_keys=32)  # ~72 MiB, staged chunks
-    _check(atls, b, 6, pinned=zero_copy)
+    _check(atls, b, 6, pinned=bool(zero_copy))
 
 
 def test_zero_copy_mixed_suites_planned(atls, monkeypatch):
