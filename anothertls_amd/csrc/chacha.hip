@@ -210,7 +210,9 @@ struct ChArgs {
 #endif
 typedef uint32_t v4u32_ch __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4u32_ch lds_uint4;
-template <bool OPEN, int G, bool LATE, bool CARRY = false, bool PRE = G == 64>
+// PRE: 0 = a slot's data is loaded where it is used (after its keystream); 1 = at the top of its step,
+// before the keystream; 2 = one step ahead, before the previous step's stores (chacha_kernel_w2).
+template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G == 64 ? 1 : 0>
 __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl,
                               lds_uint4* lds = nullptr) {
   // TLS and WIRE: nonce from (static IV, seq), 5-byte AAD; WIRE also frames the record
@@ -276,14 +278,31 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     }
   };
 
+  // PRE == 2: every lane loads 64 B per step whatever its slot (a whole block of its next slot, or the
+  // always-readable key schedule): an unconditional load keeps the compiler's s_waitcnt for the
+  // current block from waiting on the prefetch too.
+  auto blk_addr = [&](uint32_t jj) -> const uint8_t* {
+    return (jj >= 1 && jj <= jmax && 64u * (jj - 1) + 64u <= len) ? src + 64u * (jj - 1) : (const uint8_t*)k;
+  };
+  uint4 pre[4] = {};
+  if (PRE == 2) {
+    const uint8_t* a0 = blk_addr((uint32_t)gl);
+#pragma unroll
+    for (int q = 0; q < 4; q++) pre[q] = ld16(a0 + 16 * q);
+  }
   for (uint32_t base = 0; base <= jL; base += G) {
     const uint32_t j = base + (uint32_t)gl;
     const bool active = j <= jL;
     // Latency path (G = 64, one record per wave, the single call): the block's data is loaded before
     // its keystream is computed, so the load's latency (PCIe when the kernel reads pinned host
     // memory) hides under the ChaCha rounds. The throughput paths keep the registers free instead.
-    uint4 pre[4] = {};
-    if (PRE && active && j >= 1 && j <= jmax && 64u * (j - 1) + 64u <= len) {
+    uint4 nxt[4] = {};
+    if (PRE == 2) {
+      const uint8_t* an = blk_addr(j + (uint32_t)G);
+#pragma unroll
+      for (int q = 0; q < 4; q++) nxt[q] = ld16(an + 16 * q);
+    }
+    if (PRE == 1 && active && j >= 1 && j <= jmax && 64u * (j - 1) + 64u <= len) {
 #pragma unroll
       for (int q = 0; q < 4; q++) pre[q] = ld16(src + 64u * (j - 1) + 16 * q);
     }
@@ -313,6 +332,11 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       r64 = shfl_p<G>(R, G - 1);
     }
     if (!active) continue;
+    const uint4 cur0 = pre[0], cur1 = pre[1], cur2 = pre[2], cur3 = pre[3];
+    if (PRE == 2) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) pre[q] = nxt[q];  // next step's block
+    }
 
     P130 inner = p_zero();
     uint32_t cnt = 0;
@@ -365,7 +389,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         if (off + 64 <= len) {
 #pragma unroll
           for (int q = 0; q < 4; q++) {
-            const uint4 v = PRE ? pre[q] : ld16(src + off + 16 * q);
+            const uint4 v = PRE ? (q == 0 ? cur0 : q == 1 ? cur1 : q == 2 ? cur2 : cur3) : ld16(src + off + 16 * q);
             P[4 * q] = v.x; P[4 * q + 1] = v.y; P[4 * q + 2] = v.z; P[4 * q + 3] = v.w;
           }
         } else {
@@ -534,7 +558,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 
 // One group of G lanes seals / opens the record at work-list position q (direct batches: the
 // kernel validates the descriptor itself).
-template <bool OPEN, int G, bool LATE, bool CARRY = false, bool PRE = G == 64>
+template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G == 64 ? 1 : 0>
 __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W, uint32_t q, uint32_t cnt, int gl,
                                              lds_uint4* lds = nullptr) {
   if (q >= cnt) return;
@@ -590,6 +614,9 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
 #define ATLS_CHACHA_PLANNED_EARLY 0  // 1: planned seals keep r^2, r^3 live and fold full slots by SOP -- 31
                                      // spilled VGPRs at the 128 cap, C5 seal 0.327 -> 0.349 ms (ab_c35_early.log)
 #endif
+#ifndef ATLS_CHACHA_PLANNED_PRE
+#define ATLS_CHACHA_PLANNED_PRE 0  // 2: planned batches prefetch a step ahead (needs MINW_SIDE 2: ~210 VGPRs)
+#endif
 #ifndef ATLS_CHACHA_PLANNED_G
 #define ATLS_CHACHA_PLANNED_G 16  // lanes per record in planned (mixed) batches; C5 0.341 ms at 16, 0.359 at
                                   // 8, 0.435 at 4 (profiles/r02/ab_chacha_planned_g.log)
@@ -602,7 +629,8 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
   const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) / 64u;
   const uint32_t stride = gridDim.x * blockDim.x / 64u * kPer;
   for (uint32_t q0 = wave * kPer; q0 < cnt; q0 += stride)
-    chacha_group<OPEN, G, OPEN || !ATLS_CHACHA_PLANNED_EARLY>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
+    chacha_group<OPEN, G, (ATLS_CHACHA_PLANNED_EARLY | ATLS_CHACHA_PLANNED_PRE) == 0, false, ATLS_CHACHA_PLANNED_PRE>(
+        A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1));
 }
 
 // Records up to ATLS_CHACHA_TINY bytes (every record of a wave step) take ATLS_CHACHA_TINY_G
@@ -632,7 +660,11 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
 #define ATLS_CHACHA_W2 1
 #endif
 #ifndef ATLS_CHACHA_W2_PRE
-#define ATLS_CHACHA_W2_PRE 1
+#define ATLS_CHACHA_W2_PRE 2  // 1: load a slot's data at the top of its step; 2: one step ahead (C3 open 0.0962 ->
+                              // 0.0926 ms, seal 0.0834 -> 0.0806 ms: profiles/r03/ab_c3_pf.log)
+#endif
+#ifndef ATLS_CHACHA_W2_SEAL
+#define ATLS_CHACHA_W2_SEAL 1  // seals take the 2-wave kernel too (with the prefetch; with PRE = 1 they measured 3 % slower)
 #endif
 #ifndef ATLS_CHACHA_W2_EARLY
 #define ATLS_CHACHA_W2_EARLY 1  // the 2-wave kernel keeps r^2, r^3 live (not LATE), so its opens fold by SOP too:
@@ -640,7 +672,7 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
 #endif
 
 // Direct batch: P positions per wave and step, the width chosen per step from their longest record.
-template <bool OPEN, bool PRE = false>
+template <bool OPEN, int PRE = 0>
 __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
   constexpr bool LATE = OPEN && !(PRE && ATLS_CHACHA_W2_EARLY);
   __shared__ v4u32_ch carry[256 * 4];  // CARRY: 4 pieces of 16 B per lane (16 KiB per workgroup)
@@ -676,15 +708,17 @@ __global__ __launch_bounds__(256, PLANNED ? (OPEN ? ATLS_CHACHA_MINW_SIDE_OPEN :
   else chacha_direct<OPEN>(A, lane);
 }
 
-// Direct opens that give at most two waves per SIMD (C3: 65,536 MTU-sized records = 2,048 waves of 32
+// Direct batches that give at most two waves per SIMD (C3: 65,536 MTU-sized records = 2,048 waves of 32
 // records on 1,024 SIMDs) lose nothing to a 2-wave register bound, and 256 VGPRs let each lane load its
-// slot's data before computing the keystream (PRE) without spilling. The C3 kernels' waves sat at
-// s_waitcnt a quarter of their cycles (profiles/r03/c3_pmc_stall_*.csv). Same-box A/B over 3 rounds
-// (profiles/r03/ab_c3_w2.log): C3 open 0.1016 -> 0.1003 ms (0.1005 without PRE); C3 seal 0.0878 ->
-// 0.0908 ms with PRE, 0.0874 without, so seals keep the 3-wave kernel (where SOP took them to 0.0840).
+// next slot's data a step ahead (PRE == 2) and keep r^2, r^3 live for SOP without spilling. The C3
+// kernels' waves sat at s_waitcnt a quarter of their cycles (profiles/r03/c3_pmc_stall_*.csv). Same-box
+// A/Bs over 3 rounds: C3 open 0.1016 -> 0.0977 ms (data at the top of the step, SOP;
+// profiles/r03/ab_c3_w2.log, ab_c35_early.log) -> 0.0926 ms (a step ahead, ab_c3_pf.log); C3 seal 0.0834
+// (3-wave kernel, SOP) -> 0.0806 ms (2-wave kernel, a step ahead) -- loading at the top of the same step
+// had made seals 3 % slower: the wait for that block also waited for the previous step's stores.
 template <bool OPEN>
-__global__ __launch_bounds__(256, 2) void chacha_kernel_w2(ChArgs A) {  // OPEN only (launch below)
-  chacha_direct<OPEN, (bool)ATLS_CHACHA_W2_PRE>(A, threadIdx.x & 63);
+__global__ __launch_bounds__(256, 2) void chacha_kernel_w2(ChArgs A) {
+  chacha_direct<OPEN, ATLS_CHACHA_W2_PRE>(A, threadIdx.x & 63);
 }
 
 // Latency path for a few records (the Cipher-trait single call, record.rs:191-193): one record per
@@ -725,9 +759,10 @@ extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs
   } else if (idx) {
     if (open) hipLaunchKernelGGL((atls::chacha_kernel<true, true>), dim3(g), dim3(256), 0, s, A);
     else hipLaunchKernelGGL((atls::chacha_kernel<false, true>), dim3(g), dim3(256), 0, s, A);
-  } else if (ATLS_CHACHA_W2 && open && cus > 0 && (n + 31u) / 32u <= 8u * (uint32_t)cus) {
+  } else if (ATLS_CHACHA_W2 && (open || ATLS_CHACHA_W2_SEAL) && cus > 0 && (n + 31u) / 32u <= 8u * (uint32_t)cus) {
     // a wave step covers 32 positions: at most 2 waves per SIMD of work (chacha_kernel_w2)
-    hipLaunchKernelGGL((atls::chacha_kernel_w2<true>), dim3(g), dim3(256), 0, s, A);
+    if (open) hipLaunchKernelGGL((atls::chacha_kernel_w2<true>), dim3(g), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((atls::chacha_kernel_w2<false>), dim3(g), dim3(256), 0, s, A);
   } else {
     if (open) hipLaunchKernelGGL((atls::chacha_kernel<true, false>), dim3(g), dim3(256), 0, s, A);
     else hipLaunchKernelGGL((atls::chacha_kernel<false, false>), dim3(g), dim3(256), 0, s, A);

@@ -98,7 +98,7 @@ struct atls_engine {
   DevBuf grp_cnt, grp_aux, grp_idx;          // key groups of direct AES-GCM batches (plan.hip)
   uint32_t group_min = 2048;                 // ATLS_GCM_GROUP_MIN: smallest batch to group (0: never)
   int chacha_wgs = 8;                        // ATLS_CHACHA_WGS: ChaCha20-Poly1305 workgroups per CU
-  bool chacha_w2 = true;                     // ATLS_CHACHA_W2=0: direct batches never take the 2-wave kernel
+  int chacha_w2 = 1;  // ATLS_CHACHA_W2: direct batches take the 2-wave kernel when they fit (1), never (0), always (2)
   bool force_plan = false;                   // ATLS_FORCE_PLAN=1: plan every batch (tests)
   bool no_pipeline = false;                  // ATLS_NO_PIPELINE=1: stage host batches in one piece
   // Host-memory batches (run_host_pipelined): an upload and a download stream beside the engine stream,
@@ -185,6 +185,9 @@ void extents(const atls_rec* recs, uint32_t n, bool open, size_t* in_end, size_t
   *aux_end = c;
 }
 
+// The CU count atls_launch_chacha sizes its 2-wave choice by: 0 never takes it, a huge count always does.
+int w2_cus(const atls_engine* e) { return e->chacha_w2 == 0 ? 0 : e->chacha_w2 == 2 ? (1 << 26) : e->cus; }
+
 int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n, const uint8_t* d_in,
                    const uint8_t* d_aux, uint8_t* d_out, uint8_t* d_tags_out, const uint8_t* d_tags_in,
                    atls_open_result* d_res, hipStream_t s, uint32_t* done = nullptr, uint32_t done_val = 0) {
@@ -192,7 +195,7 @@ int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n
   if (e->has_chacha)
     return atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, nullptr,
                               nullptr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, s, done, done_val,
-                              e->chacha_w2 ? e->cus : 0);
+                              w2_cus(e));
   return atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, nullptr, nullptr, (uint32_t*)e->err.p, e->n_slots,
                          e->aes_nr_mask, nullptr, nullptr, e->cus, s, done, done_val);
@@ -441,7 +444,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     }
     rc = atls_launch_chacha(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res, idx,
                             plan_hdr, (uint32_t*)e->err.p, e->n_slots, e->cus * e->chacha_wgs, cs, nullptr, 0,
-                            e->chacha_w2 ? e->cus : 0);
+                            w2_cus(e));
     if (rc) return rc;
     if (side && hipEventRecord(ps.side_done, e->stream2) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
@@ -841,7 +844,7 @@ atls_engine* atls_engine_create(int device) {
   if (const char* v = std::getenv("ATLS_FORCE_PLAN")) e->force_plan = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_NO_PIPELINE")) e->no_pipeline = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_CHACHA_WGS")) e->chacha_wgs = std::max(1, std::atoi(v));
-  if (const char* v = std::getenv("ATLS_CHACHA_W2")) e->chacha_w2 = std::atoi(v) != 0;
+  if (const char* v = std::getenv("ATLS_CHACHA_W2")) e->chacha_w2 = std::atoi(v);
   if (const char* v = std::getenv("ATLS_ZERO_COPY")) e->zero_copy = std::atoi(v);
   if (const char* v = std::getenv("ATLS_GCM_GROUP_MIN")) e->group_min = (uint32_t)std::max(0, std::atoi(v));
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || hipMemsetAsync(e->err.p, 0, 16, e->stream) != hipSuccess ||

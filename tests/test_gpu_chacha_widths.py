@@ -3,8 +3,8 @@ consecutive records and runs them 2 lanes per record when all are tiny (<= ATLS_
 B), else 4 lanes per record in two rounds when all are short (<= ATLS_CHACHA_SHORT = 4096 B), else
 16 lanes per record in eight rounds (the third case below puts one long record among short ones,
 so two widths run in one launch); a batch of at most ATLS_CHACHA_LAT_MAX = 32 records (the single
-call) runs one record per wave at 64 lanes (chacha_kernel_lat, the fourth case); each case's opens run
-on the 2-wave and on the 3-wave direct kernel (ATLS_CHACHA_W2); all are
+call) runs one record per wave at 64 lanes (chacha_kernel_lat, the fourth case); each case runs on the
+2-wave and on the 3-wave direct kernel (ATLS_CHACHA_W2); all are
 checked against the oracle on the lengths that exercise the per-lane Poly1305 combine and the
 reference's F4 quirk (ChaCha20::encrypt leaves the last block unencrypted when len % 64 == 0,
 crypto/chacha20/cipher.rs:99-102), sealed and reopened, with tampered tags."""
@@ -32,9 +32,9 @@ def atls():
 @pytest.mark.parametrize("lens", [TINY * 20, SHORT * 20, SHORT * 20 + [16384], SHORT + [16383, 16384, 5000]],
                          ids=["all-tiny-2-lanes", "all-short-4-lanes", "one-long-16-lanes", "few-records-64-lanes"])
 def test_chacha_widths_vs_oracle(atls, lens, w2, monkeypatch):
-    """w2: direct opens of at most two waves per SIMD take chacha_kernel_w2 (256 VGPRs, data loaded
-    before the keystream); ATLS_CHACHA_W2=0 sends them to the 3-wave chacha_kernel that seals and larger
-    batches take, so both direct open kernels see every width."""
+    """w2: direct batches of at most two waves per SIMD take chacha_kernel_w2 (256 VGPRs, each slot's
+    data loaded a step ahead); ATLS_CHACHA_W2=0 sends them to the 3-wave chacha_kernel that larger
+    batches take, so both direct kernels see every width."""
     from anothertls_amd import workload
 
     monkeypatch.setenv("ATLS_CHACHA_W2", w2)
