@@ -202,6 +202,10 @@ struct ChArgs {
 // (profiles/r03/ab_chacha_mac_first.log): C5 open kernel 0.320 -> 0.306 ms, C3 open 0.1010 -> 0.0994 ms;
 // a 3-wave bound for the planned open instead (152 VGPRs, no spills) fixed the traffic but not the
 // time (0.325 ms: no wave of it fits beside an AES-GCM workgroup).
+#ifndef ATLS_CHACHA_DBG
+#define ATLS_CHACHA_DBG 0  // timing builds only (wrong results): 1 = no keystream for data slots, 2 = no MAC of
+                           // full seal slots, 4 = no loads or stores of full blocks (PRE >= 2 kernels)
+#endif
 #ifndef ATLS_CHACHA_SOP
 #define ATLS_CHACHA_SOP 1
 #endif
@@ -278,17 +282,23 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     }
   };
 
-  // PRE == 2: every lane loads 64 B per step whatever its slot (a whole block of its next slot, or the
-  // always-readable key schedule): an unconditional load keeps the compiler's s_waitcnt for the
-  // current block from waiting on the prefetch too.
+  // PRE >= 2: every lane loads 64 B per step whatever its slot (a whole block of the slot PRE - 1 steps
+  // ahead, or the always-readable key schedule): an unconditional load keeps the compiler's s_waitcnt
+  // for the current block from waiting on the prefetches too. ring[0] is the current step's block.
   auto blk_addr = [&](uint32_t jj) -> const uint8_t* {
-    return (jj >= 1 && jj <= jmax && 64u * (jj - 1) + 64u <= len) ? src + 64u * (jj - 1) : (const uint8_t*)k;
+    return (!(ATLS_CHACHA_DBG & 4) && jj >= 1 && jj <= jmax && 64u * (jj - 1) + 64u <= len) ? src + 64u * (jj - 1)
+                                                                                             : (const uint8_t*)k;
   };
-  uint4 pre[4] = {};
-  if (PRE == 2) {
-    const uint8_t* a0 = blk_addr((uint32_t)gl);
+  constexpr int NR = PRE >= 2 ? PRE - 1 : 1;
+  uint4 ring[NR][4] = {};
+  uint4 (&pre)[4] = ring[0];
+  if (PRE >= 2) {
 #pragma unroll
-    for (int q = 0; q < 4; q++) pre[q] = ld16(a0 + 16 * q);
+    for (int i = 0; i < NR; i++) {
+      const uint8_t* a0 = blk_addr((uint32_t)gl + (uint32_t)(i * G));
+#pragma unroll
+      for (int q = 0; q < 4; q++) ring[i][q] = ld16(a0 + 16 * q);
+    }
   }
   for (uint32_t base = 0; base <= jL; base += G) {
     const uint32_t j = base + (uint32_t)gl;
@@ -297,8 +307,8 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     // its keystream is computed, so the load's latency (PCIe when the kernel reads pinned host
     // memory) hides under the ChaCha rounds. The throughput paths keep the registers free instead.
     uint4 nxt[4] = {};
-    if (PRE == 2) {
-      const uint8_t* an = blk_addr(j + (uint32_t)G);
+    if (PRE >= 2) {
+      const uint8_t* an = blk_addr(j + (uint32_t)(NR * G));
 #pragma unroll
       for (int q = 0; q < 4; q++) nxt[q] = ld16(an + 16 * q);
     }
@@ -307,7 +317,14 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       for (int q = 0; q < 4; q++) pre[q] = ld16(src + 64u * (j - 1) + 16 * q);
     }
     uint32_t ks[16];
-    if (active && j <= jmax && (!MAC_FIRST || j == 0)) chacha_block(kw, j, nw, ks);
+    if (active && j <= jmax && (!MAC_FIRST || j == 0)) {
+      if ((ATLS_CHACHA_DBG & 1) && j) {  // timing build: no keystream for data slots (wrong output)
+#pragma unroll
+        for (int q = 0; q < 16; q++) ks[q] = kw[q & 7] ^ j;
+      } else {
+        chacha_block(kw, j, nw, ks);
+      }
+    }
     if (base == 0) {
       // Poly1305 one-time key from block 0 (poly1305.rs:19-22), broadcast within the group.
       uint32_t r0 = __shfl(ks[0], 0, G), r1 = __shfl(ks[1], 0, G), r2 = __shfl(ks[2], 0, G), r3 = __shfl(ks[3], 0, G);
@@ -333,9 +350,13 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     }
     if (!active) continue;
     const uint4 cur0 = pre[0], cur1 = pre[1], cur2 = pre[2], cur3 = pre[3];
-    if (PRE == 2) {
+    if (PRE >= 2) {
 #pragma unroll
-      for (int q = 0; q < 4; q++) pre[q] = nxt[q];  // next step's block
+      for (int i = 0; i + 1 < NR; i++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) ring[i][q] = ring[i + 1][q];
+#pragma unroll
+      for (int q = 0; q < 4; q++) ring[NR - 1][q] = nxt[q];  // the block PRE - 1 steps ahead
     }
 
     P130 inner = p_zero();
@@ -434,7 +455,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
               cmask |= 1u << q;
               coff = off;
             } else {
-              st16(dst + off + 16 * q, v);
+              if (!(ATLS_CHACHA_DBG & 4)) st16(dst + off + 16 * q, v);
             }
           }
         } else {
@@ -453,7 +474,8 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
             }
           }
         } else if (SOP && valid == 64u) {
-          p_sop4(acc, base == 0, r64, P, r, rsq, rcu);  // seal: the MAC over the ciphertext just written
+          if (ATLS_CHACHA_DBG & 2) acc.l[0] ^= P[0] ^ P[5] ^ P[10] ^ P[15];  // timing build: no MAC (wrong tags)
+          else p_sop4(acc, base == 0, r64, P, r, rsq, rcu);  // seal: the MAC over the ciphertext just written
           sop = true;
         } else {
           fold(P);  // seal: the MAC runs over the ciphertext just written
@@ -615,7 +637,9 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
                                      // spilled VGPRs at the 128 cap, C5 seal 0.327 -> 0.349 ms (ab_c35_early.log)
 #endif
 #ifndef ATLS_CHACHA_PLANNED_PRE
-#define ATLS_CHACHA_PLANNED_PRE 0  // 2: planned batches prefetch a step ahead (needs MINW_SIDE 2: ~210 VGPRs)
+#define ATLS_CHACHA_PLANNED_PRE 0  // 2: planned batches prefetch a step ahead with early powers (180 VGPRs, so
+                                   // MINW_SIDE 2 or 3): C5 seal 0.325 -> 0.334 ms, open 0.310 -> 0.329 ms
+                                   // (profiles/r03/ab_c5_planned_pf.log); off
 #endif
 #ifndef ATLS_CHACHA_PLANNED_G
 #define ATLS_CHACHA_PLANNED_G 16  // lanes per record in planned (mixed) batches; C5 0.341 ms at 16, 0.359 at
@@ -739,6 +763,8 @@ __global__ __launch_bounds__(64) void chacha_kernel_lat(ChArgs A) {
 }
 
 }  // namespace atls
+
+extern "C" unsigned atls_chacha_dbg(void) { return ATLS_CHACHA_DBG; }
 
 // idx / plan: the batch plan's work lists (G = 16), or nullptr for a direct batch (per-step widths).
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,

@@ -1044,9 +1044,10 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
 
 // Compile-time experiment switches this library was built with (include/atls.h
 // atls_build_flags): 0 for the product build, which must compute the reference's results.
+extern "C" unsigned atls_chacha_dbg(void);  // chacha.hip: its timing-build switch (ATLS_CHACHA_DBG)
 extern "C" unsigned atls_build_flags(void) {
   unsigned f = 0;
-  if (ATLS_DBG_SKIP) f |= ATLS_BUILD_DBG_SKIP;
+  if (ATLS_DBG_SKIP || atls_chacha_dbg()) f |= ATLS_BUILD_DBG_SKIP;
   if (ATLS_DBG_SHARED_GHASH) f |= ATLS_BUILD_DBG_SHARED_GHASH;
   if (ATLS_GHASH_W) f |= ATLS_BUILD_GHASH_W;
   if (!ATLS_CTR_CACHE) f |= ATLS_BUILD_NO_CTR_CACHE;
