@@ -48,6 +48,12 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* p) {
   return v;
 }
 __device__ __forceinline__ void st16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
+__device__ __forceinline__ uint32_t ld4(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);
+  return v;
+}
+__device__ __forceinline__ void st4(uint8_t* p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
 
 // RecordType::new (net/record.rs:22-33): Invalid(0), ChangeCipherSpec, Alert, Handshake,
 // ApplicationData.

@@ -414,13 +414,23 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
             P[4 * q] = v.x; P[4 * q + 1] = v.y; P[4 * q + 2] = v.z; P[4 * q + 3] = v.w;
           }
         } else {
+          // a partial block, word by word (compile-time word index: P stays in registers): a word wholly
+          // inside the input is one 4-byte load, the word holding the input's end is assembled from
+          // bytes and the content type (record.rs:173); words past `valid` stay zero
 #pragma unroll
-          for (int q = 0; q < 16; q++) P[q] = 0;
+          for (int w = 0; w < 16; w++) {
+            P[w] = 0;
+            const uint32_t b0 = 4u * (uint32_t)w;
+            if (b0 < valid) {
+              if (off + b0 + 4u <= len) {
+                P[w] = ld4(src + off + b0);
+              } else {
 #pragma unroll
-          for (int q = 0; q < 64; q++) {  // compile-time byte index: P stays in registers
-            if ((uint32_t)q < valid) {
-              const uint32_t byte = (off + q < len) ? src[off + q] : (uint32_t)d.content_type;  // record.rs:173
-              P[q >> 2] |= byte << (8 * (q & 3));
+                for (int q = 0; q < 4; q++)
+                  if (b0 + (uint32_t)q < valid)
+                    P[w] |= ((off + b0 + (uint32_t)q < len) ? (uint32_t)src[off + b0 + q] : (uint32_t)d.content_type)
+                            << (8 * q);
+              }
             }
           }
         }
@@ -460,8 +470,16 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
           }
         } else {
 #pragma unroll
-          for (int q = 0; q < 64; q++)
-            if ((uint32_t)q < valid) dst[off + q] = (uint8_t)(P[q >> 2] >> (8 * (q & 3)));
+          for (int w = 0; w < 16; w++) {  // word by word, bytes only for the word holding the end
+            const uint32_t b0 = 4u * (uint32_t)w;
+            if (b0 + 4u <= valid) {
+              st4(dst + off + b0, P[w]);
+            } else if (b0 < valid) {
+#pragma unroll
+              for (int q = 0; q < 4; q++)
+                if (b0 + (uint32_t)q < valid) dst[off + b0 + q] = (uint8_t)(P[w] >> (8 * q));
+            }
+          }
         }
         if (OPEN) {
           if (tls) {
