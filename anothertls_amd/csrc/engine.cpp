@@ -235,6 +235,14 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   for (uint32_t i = 1; i < n && pitched; i++)
     pitched = olen(recs[i]) == width && recs[i].out_off == recs[0].out_off + i * pitch;
   hipStream_t ks = e->stream, up = e->up, down = e->down;
+  // A failure after work is queued returns only once the queued copies and kernels are done with the
+  // caller's buffers (nothing may write them after the call returns).
+  auto fail = [&](int rc) {
+    (void)hipStreamSynchronize(up);
+    (void)hipStreamSynchronize(ks);
+    (void)hipStreamSynchronize(down);
+    return rc;
+  };
   // ATLS_ZERO_COPY=2: the kernels write their output (records, tags, open results) straight into the
   // page-locked host buffers, so nothing comes back through the download stream and nothing of `out`
   // is staged in (only record bytes are written); the inputs still go up in chunks.
@@ -251,9 +259,9 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   const bool zo = z_out != nullptr;
   // the batch's descriptors and aux are in place, and the engine's earlier batches (which used the same
   // staging buffers) are done, before the first upload
-  if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, ks) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, ks) != hipSuccess) return fail(ATLS_INTERNAL_ERROR);
   if (hipEventRecord(e->ev_plan, ks) != hipSuccess || hipStreamWaitEvent(up, e->ev_plan, 0) != hipSuccess)
-    return ATLS_INTERNAL_ERROR;
+    return fail(ATLS_INTERNAL_ERROR);
   const auto* d_recs = (const atls_rec*)e->recs.p;
   auto* d_in = (uint8_t*)e->in.p;
   auto* d_out = (uint8_t*)e->out.p;
@@ -267,7 +275,7 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
     while (b < n && recs[b - 1].in_off + ilen(recs[b - 1]) - recs[a].in_off < kChunkBytes) b++;
     while (e->pev.size() < 2 * (k + 1)) {
       hipEvent_t ev;
-      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return ATLS_INTERNAL_ERROR;
+      if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail(ATLS_INTERNAL_ERROR);
       e->pev.push_back(ev);
     }
     hipEvent_t uploaded = e->pev[2 * k], sealed = e->pev[2 * k + 1];
@@ -276,43 +284,43 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
     const uint32_t cnt = b - a;
     if (in_hi > in_lo &&
         hipMemcpyAsync(d_in + in_lo, (const uint8_t*)in + in_lo, in_hi - in_lo, hipMemcpyHostToDevice, up) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
     if (open && tags_in && hipMemcpyAsync(d_tags + 16 * (size_t)a, tags_in + 16 * (size_t)a, 16 * (size_t)cnt,
                                hipMemcpyHostToDevice, up) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
     if (!zo && !pitched && out_hi > out_lo &&
         hipMemcpyAsync(d_out + out_lo, (uint8_t*)out + out_lo, out_hi - out_lo, hipMemcpyHostToDevice, up) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
     if (hipEventRecord(uploaded, up) != hipSuccess || hipStreamWaitEvent(ks, uploaded, 0) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
     uint8_t* k_tags_out = d_tags + 16 * (size_t)a;
     if (zo && !open) k_tags_out = z_tags ? z_tags + 16 * (size_t)a : k_tags_out;
     int rc = launch_records(e, open, d_recs + a, cnt, d_in, (const uint8_t*)e->aux.p, zo ? z_out : d_out, k_tags_out,
                             d_tags + 16 * (size_t)a, zo && open ? z_res + a : d_res + a, ks);
-    if (rc) return rc;
+    if (rc) return fail(rc);
     const uint32_t a0 = a;
     a = b;
     if (zo) continue;  // written in place
     if (hipEventRecord(sealed, ks) != hipSuccess || hipStreamWaitEvent(down, sealed, 0) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
     if (pitched) {
       if (width && hipMemcpy2DAsync((uint8_t*)out + out_lo, pitch, d_out + out_lo, pitch, width, cnt,
                                     hipMemcpyDeviceToHost, down) != hipSuccess)
-        return ATLS_INTERNAL_ERROR;
+        return fail(ATLS_INTERNAL_ERROR);
     } else if (out_hi > out_lo &&
                hipMemcpyAsync((uint8_t*)out + out_lo, d_out + out_lo, out_hi - out_lo, hipMemcpyDeviceToHost, down) != hipSuccess) {
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
     }
     if (!open && tags_out && hipMemcpyAsync(tags_out + 16 * (size_t)a0, d_tags + 16 * (size_t)a0, 16 * (size_t)cnt,
                                 hipMemcpyDeviceToHost, down) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
     if (open && hipMemcpyAsync(res + a0, d_res + a0, sizeof(atls_open_result) * (size_t)cnt, hipMemcpyDeviceToHost, down) !=
                     hipSuccess)
-      return ATLS_INTERNAL_ERROR;
+      return fail(ATLS_INTERNAL_ERROR);
   }
   // the engine stream is ordered after the last download (finish synchronises it)
   if (!zo && (hipEventRecord(e->ev_side, down) != hipSuccess || hipStreamWaitEvent(ks, e->ev_side, 0) != hipSuccess))
-    return ATLS_INTERNAL_ERROR;
+    return fail(ATLS_INTERNAL_ERROR);
   return finish(e, 0);
 }
 
