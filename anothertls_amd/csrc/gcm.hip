@@ -40,6 +40,12 @@ namespace atls {
                          // table, 8 GHASH multiply in general steps, 16 last step, 32 first step,
                          // 64 the last AES round's lookups
 #endif
+#ifndef ATLS_GEN_VEC
+#define ATLS_GEN_VEC 0  // general steps: whole blocks of unaligned records by 16-byte accesses too (ld16 / st16).
+                        // C5's general steps cost 12 % of its kernel interval (timing build ATLS_DBG_SKIP=2,
+                        // profiles/r03/ab_c5_gcm_parts.log), but not through their byte accesses: C5 0.322 vs
+                        // 0.323 ms, C2 unchanged (ab_gcm_general_vec.log, parity per variant); off
+#endif
 #ifndef ATLS_CTR_CACHE
 #define ATLS_CTR_CACHE 1
 #endif
@@ -478,8 +484,8 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     const uint32_t g = s - 1;
     if (s >= 1 && s <= m && g >= na && g < na + nb) {
       const uint32_t off = (g - na) * 16;
-      if (off + 16 <= in_bytes && src_al) {
-        const uint4 v = *reinterpret_cast<const uint4*>(src + off);
+      if (off + 16 <= in_bytes && (ATLS_GEN_VEC || src_al)) {
+        const uint4 v = ATLS_GEN_VEC ? ld16(src + off) : *reinterpret_cast<const uint4*>(src + off);
         P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
       } else {
         const uint32_t valid = min(16u, n_aead - off);
@@ -522,8 +528,9 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
             if ((int)valid < lo + 4) C[w] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
           }
         }
-        if (valid == 16 && dst_al) {
-          *reinterpret_cast<uint4*>(dst + off) = make_uint4(C[0], C[1], C[2], C[3]);
+        if (valid == 16 && (ATLS_GEN_VEC || dst_al)) {
+          if (ATLS_GEN_VEC) st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
+          else *reinterpret_cast<uint4*>(dst + off) = make_uint4(C[0], C[1], C[2], C[3]);
         } else {
 #pragma unroll
           for (int q = 0; q < 16; q++)
@@ -803,8 +810,8 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
     uint32_t P[4] = {0, 0, 0, 0};
     if (data) {
       const uint32_t off = (s - 2u) * 16u;
-      if (off + 16u <= len && src_al) {
-        const uint4 v = *reinterpret_cast<const uint4*>(src + off);
+      if (off + 16u <= len && (ATLS_GEN_VEC || src_al)) {
+        const uint4 v = ATLS_GEN_VEC ? ld16(src + off) : *reinterpret_cast<const uint4*>(src + off);
         P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
       } else {
         const uint32_t valid = min(16u, n_aead - off);
@@ -836,8 +843,9 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
           if ((int)valid < lo + 4) C[w] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - valid)));
         }
       }
-      if (valid == 16 && dst_al) {
-        *reinterpret_cast<uint4*>(dst + off) = make_uint4(C[0], C[1], C[2], C[3]);
+      if (valid == 16 && (ATLS_GEN_VEC || dst_al)) {
+        if (ATLS_GEN_VEC) st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
+        else *reinterpret_cast<uint4*>(dst + off) = make_uint4(C[0], C[1], C[2], C[3]);
       } else {
 #pragma unroll
         for (int q = 0; q < 16; q++)
