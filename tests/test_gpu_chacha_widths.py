@@ -68,3 +68,37 @@ def test_chacha_widths_vs_oracle(atls, lens, w2, monkeypatch):
         o, io, L = int(r2["out_off"][i]), int(recs["in_off"][i]), int(recs["len"][i])
         assert np.array_equal(pt[o:o + L], inbuf[io:io + L]), i
     eng.close()
+
+
+@pytest.mark.parametrize("w2", ["1", "2"], ids=["past-2-waves-3-wave-kernel", "forced-2-wave-kernel"])
+def test_chacha_direct_batch_past_two_waves_per_simd(atls, w2, monkeypatch):
+    """A direct batch one wave step larger than two waves per SIMD of work (8 x CUs x 32 records + 32)
+    leaves chacha_kernel_w2 for the 3-wave chacha_kernel (ATLS_CHACHA_W2=1); ATLS_CHACHA_W2=2 keeps the
+    2-wave kernel at that size, its waves then taking several wave steps each. Both against the oracle."""
+    import torch
+    from anothertls_amd import workload
+
+    monkeypatch.setenv("ATLS_CHACHA_W2", w2)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = 8 * cus * 32 + 32
+    lens = np.random.default_rng(n).integers(0, 200, n).astype(np.uint64)
+    b = workload.tls_batch(n, lens, 0x1303, n_keys=97)
+    recs = b["recs"]
+    inbuf = np.random.default_rng(1).integers(0, 256, b["in_bytes"] + 16, dtype=np.uint8)
+    eng = atls.Engine(0)
+    eng.set_keys(b["keys"])
+    out = np.zeros(b["out_bytes"] + 16, np.uint8)
+    tags = np.zeros(16 * n, np.uint8)
+    eng.seal_batch(recs, inbuf, np.zeros(16, np.uint8), out, tags)
+    okeys = (ora.OraKey * len(b["keys"])).from_buffer_copy(b["keys"].tobytes())
+    orecs = (ora.OraRec * n).from_buffer_copy(recs.tobytes())
+    oout, otags = np.zeros_like(out), np.zeros_like(tags)
+    assert ora.seal_batch(okeys, orecs, inbuf, np.zeros(16, np.uint8), oout, otags, 8) == 0
+    assert np.array_equal(out, oout) and np.array_equal(tags, otags)
+    r2 = recs.copy()
+    r2["in_off"], r2["len"] = recs["out_off"], recs["len"] + 1
+    pt = np.zeros_like(out)
+    res = np.zeros(n, atls.OPEN_RESULT_DTYPE)
+    eng.open_batch(r2, out, np.zeros(16, np.uint8), tags, pt, res)
+    assert (res["status"] == 0).all() and (res["content_len"] == recs["len"]).all()
+    eng.close()
