@@ -209,6 +209,10 @@ struct ChArgs {
 #ifndef ATLS_CHACHA_SOP
 #define ATLS_CHACHA_SOP 1
 #endif
+#ifndef ATLS_CHACHA_W2_MAC_FIRST
+#define ATLS_CHACHA_W2_MAC_FIRST 0  // 0: the 2-wave kernel's opens compute the keystream first (it has the registers):
+                                    // C3 open 0.0942 -> 0.0896 ms (profiles/r03/ab_c3_open2.log, ab_c3_open.log)
+#endif
 #ifndef ATLS_CHACHA_OPEN_MAC_FIRST
 #define ATLS_CHACHA_OPEN_MAC_FIRST 2
 #endif
@@ -266,7 +270,8 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   uint32_t sk[4] = {0, 0, 0, 0};
   P130 acc = p_zero(), innerL = p_zero();
   int64_t lastnz = -1;
-  constexpr bool MAC_FIRST = OPEN && G != 64 && (CARRY ? ATLS_CHACHA_OPEN_MAC_FIRST >= 2 : ATLS_CHACHA_OPEN_MAC_FIRST >= 1);
+  constexpr bool MAC_FIRST = OPEN && G != 64 && (PRE < 2 || ATLS_CHACHA_W2_MAC_FIRST) &&
+                             (CARRY ? ATLS_CHACHA_OPEN_MAC_FIRST >= 2 : ATLS_CHACHA_OPEN_MAC_FIRST >= 1);
   constexpr bool SOP = ATLS_CHACHA_SOP && !LATE;  // full slots: one reduction (p_sop4)
   const uint32_t mis = CARRY ? (uint32_t)((reinterpret_cast<uintptr_t>(dst) - 64u) & 127u) : 0u;
   uint32_t cmask = 0, coff = 0;  // CARRY: pieces of the block at record offset coff waiting in LDS
@@ -697,6 +702,13 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
 #ifndef ATLS_CHACHA_CARRY_SEAL
 #define ATLS_CHACHA_CARRY_SEAL 0
 #endif
+#ifndef ATLS_CHACHA_CARRY_OPEN
+#define ATLS_CHACHA_CARRY_OPEN 1
+#endif
+#ifndef ATLS_CHACHA_W2_CARRY_OPEN
+#define ATLS_CHACHA_W2_CARRY_OPEN 0  // the 2-wave kernel's opens without the carry: C3 open 0.0896 -> 0.0849 ms
+                                     // (traffic 1.17x -> 1.33x; profiles/r03/ab_c3_open2.log)
+#endif
 
 #ifndef ATLS_CHACHA_W2
 #define ATLS_CHACHA_W2 1
@@ -732,13 +744,13 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
     mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
     if (ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY) {
       constexpr int G = ATLS_CHACHA_TINY ? ATLS_CHACHA_TINY_G : 4;
-      chacha_group<OPEN, G, LATE, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
+      chacha_group<OPEN, G, LATE, (OPEN ? (PRE >= 2 ? ATLS_CHACHA_W2_CARRY_OPEN : ATLS_CHACHA_CARRY_OPEN) : ATLS_CHACHA_CARRY_SEAL), PRE>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
     } else if (mx <= (uint32_t)ATLS_CHACHA_SHORT) {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, LATE, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3, lds);
+      for (uint32_t rr = 0; rr < P / 16u; rr++) chacha_group<OPEN, 4, LATE, (OPEN ? (PRE >= 2 ? ATLS_CHACHA_W2_CARRY_OPEN : ATLS_CHACHA_CARRY_OPEN) : ATLS_CHACHA_CARRY_SEAL), PRE>(A, W, q0 + 16u * rr + (uint32_t)lane / 4u, cnt, lane & 3, lds);
     } else {
 #pragma unroll 1
-      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, LATE, OPEN || ATLS_CHACHA_CARRY_SEAL, PRE>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15, lds);
+      for (uint32_t rr = 0; rr < P / 4u; rr++) chacha_group<OPEN, 16, LATE, (OPEN ? (PRE >= 2 ? ATLS_CHACHA_W2_CARRY_OPEN : ATLS_CHACHA_CARRY_OPEN) : ATLS_CHACHA_CARRY_SEAL), PRE>(A, W, q0 + 4u * rr + (uint32_t)lane / 16u, cnt, lane & 15, lds);
     }
   }
 }
