@@ -18,6 +18,16 @@ case ${1:-A} in
     run c1 300 python bench.py --config c1_server_https_loopback_1MiB --steps 20
     run single 300 python tools/single_call_latency.py
     ;;
+  C)  # C2 / C4 / C5 bench lines and their rocprof stats + FETCH / WRITE PMC on the same box
+    run c2 400 python bench.py --pcie --wire
+    run c4 300 python bench.py --config c4_aes256gcm_1Mi_x_16KiB --no-cpu-baseline
+    run c5 300 python bench.py --config c5_mixed_256Ki_x_64B-16KiB --no-cpu-baseline
+    for c in c2:c2_aes128gcm_64Ki_x_16KiB c4:c4_aes256gcm_1Mi_x_16KiB c5:c5_mixed_256Ki_x_64B-16KiB; do
+      bash tools/profile_round.sh ${c#*:} ${c%%:*} || exit 1
+    done
+    bash tools/pmc_stall.sh c2_aes128gcm_64Ki_x_16KiB > $O/pmc_c2.log 2>&1 || { echo "pmc rc=$?"; exit 1; }
+    echo "C done"
+    ;;
   B)
     bash tools/profile_round.sh c3_chacha20poly1305_64Ki_x_1.5KiB c3 || exit 1
     bash tools/pmc_stall.sh c3_chacha20poly1305_64Ki_x_1.5KiB > $O/pmc_c3.log 2>&1 || { echo "pmc rc=$?"; exit 1; }
