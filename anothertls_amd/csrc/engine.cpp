@@ -98,7 +98,11 @@ struct atls_engine {
   DevBuf grp_cnt, grp_aux, grp_idx;          // key groups of direct AES-GCM batches (plan.hip)
   uint32_t group_min = 2048;                 // ATLS_GCM_GROUP_MIN: smallest batch to group (0: never)
   int chacha_wgs = 8;                        // ATLS_CHACHA_WGS: ChaCha20-Poly1305 workgroups per CU
-  int chacha_w2 = 1;  // ATLS_CHACHA_W2: direct batches take the 2-wave kernel when they fit (1), never (0), always (2)
+  // ATLS_CHACHA_W2: direct ChaCha20-Poly1305 batches take the 2-wave kernel always (2, the default), only when
+  // they fit in two waves per SIMD (1), never (0). Batches of 2x and 4x C3's records: 2-wave seal 0.180 /
+  // 0.369 ms against 0.202 / 0.391 for the 3-wave kernel, opens 0.186 / 0.381 against 0.202 / 0.390
+  // (profiles/r03/ab_c3_big_batches.log).
+  int chacha_w2 = 2;
   bool force_plan = false;                   // ATLS_FORCE_PLAN=1: plan every batch (tests)
   bool no_pipeline = false;                  // ATLS_NO_PIPELINE=1: stage host batches in one piece
   // Host-memory batches (run_host_pipelined): an upload and a download stream beside the engine stream,

@@ -32,9 +32,8 @@ def atls():
 @pytest.mark.parametrize("lens", [TINY * 20, SHORT * 20, SHORT * 20 + [16384], SHORT + [16383, 16384, 5000]],
                          ids=["all-tiny-2-lanes", "all-short-4-lanes", "one-long-16-lanes", "few-records-64-lanes"])
 def test_chacha_widths_vs_oracle(atls, lens, w2, monkeypatch):
-    """w2: direct batches of at most two waves per SIMD take chacha_kernel_w2 (256 VGPRs, each slot's
-    data loaded a step ahead); ATLS_CHACHA_W2=0 sends them to the 3-wave chacha_kernel that larger
-    batches take, so both direct kernels see every width."""
+    """w2: direct batches take chacha_kernel_w2 (256 VGPRs, each slot's data loaded a step ahead);
+    ATLS_CHACHA_W2=0 sends them to the 3-wave chacha_kernel, so both direct kernels see every width."""
     from anothertls_amd import workload
 
     monkeypatch.setenv("ATLS_CHACHA_W2", w2)
@@ -70,11 +69,11 @@ def test_chacha_widths_vs_oracle(atls, lens, w2, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("w2", ["1", "2"], ids=["past-2-waves-3-wave-kernel", "forced-2-wave-kernel"])
+@pytest.mark.parametrize("w2", ["1", "2"], ids=["past-2-waves-3-wave-kernel", "default-2-wave-kernel"])
 def test_chacha_direct_batch_past_two_waves_per_simd(atls, w2, monkeypatch):
     """A direct batch one wave step larger than two waves per SIMD of work (8 x CUs x 32 records + 32)
-    leaves chacha_kernel_w2 for the 3-wave chacha_kernel (ATLS_CHACHA_W2=1); ATLS_CHACHA_W2=2 keeps the
-    2-wave kernel at that size, its waves then taking several wave steps each. Both against the oracle."""
+    leaves chacha_kernel_w2 for the 3-wave chacha_kernel under ATLS_CHACHA_W2=1; the default (2) keeps the
+    2-wave kernel at every size, its waves then taking several wave steps each. Both against the oracle."""
     import torch
     from anothertls_amd import workload
 
