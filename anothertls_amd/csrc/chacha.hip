@@ -14,6 +14,10 @@
 // (ciphertext, then the length block) are Horner-folded with r; slots of one lane are folded
 // with r^(4G) = r^64; each lane's partial is finally multiplied by r^e (e in 1..65, square-
 // and-multiply over r^(2^b)) and the group sums the partials mod p.
+// Kernels: chacha_kernel_w2 (direct batches, the default: 2 waves per SIMD, each slot's block loaded a
+// step ahead, full slots' MACs folded in one reduction), chacha_kernel<OPEN, false> (direct batches under
+// ATLS_CHACHA_W2=0/1, 3 waves per SIMD), chacha_kernel<OPEN, true> (planned mixed batches beside the
+// AES-GCM kernel, 128 VGPRs), chacha_kernel_lat (the single call, one record per wave at 64 lanes).
 // Bytes per record (roofline): read L, write L + 16.
 #include "plan.h"
 
