@@ -28,7 +28,9 @@
 extern "C" int atls_launch_build_t0(uint32_t* t0, hipStream_t s);
 extern "C" int atls_launch_aes_blocks(int decrypt, const void* ks, const uint8_t* in, uint8_t* out, uint64_t nblocks,
                                       uint32_t* err, int grid, hipStream_t s);
-extern "C" int atls_launch_key_setup(const atls_key* keys, uint32_t n, void* ks, hipStream_t s);
+extern "C" int atls_launch_key_setup(const atls_key* keys, const atls_key* host_keys, uint32_t n, void* ks,
+                                     hipStream_t s);
+extern "C" int atls_key_setup_inline_max(void);
 extern "C" int atls_launch_plan(int open, const void* ks, const atls_rec* recs, uint32_t n, uint32_t n_slots,
                                 atls_open_result* res, uint32_t* err, void* P, uint8_t* keys, uint32_t* idx,
                                 uint32_t* wg, int cus, hipStream_t s);
@@ -231,9 +233,15 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   for (uint32_t i = 1; i < n; i++)
     if (recs[i].in_off < recs[i - 1].in_off + ilen(recs[i - 1]) || recs[i].out_off < recs[i - 1].out_off + olen(recs[i - 1]))
       return -1;
-  if (!e->up && (hipStreamCreateWithFlags(&e->up, hipStreamNonBlocking) != hipSuccess ||
-                 hipStreamCreateWithFlags(&e->down, hipStreamNonBlocking) != hipSuccess))
+  // each stream on its own: a failed creation of one leaves it null and is retried by the next batch
+  if (!e->up && hipStreamCreateWithFlags(&e->up, hipStreamNonBlocking) != hipSuccess) {
+    e->up = nullptr;
     return ATLS_INTERNAL_ERROR;
+  }
+  if (!e->down && hipStreamCreateWithFlags(&e->down, hipStreamNonBlocking) != hipSuccess) {
+    e->down = nullptr;
+    return ATLS_INTERNAL_ERROR;
+  }
   bool pitched = n > 1;
   const size_t pitch = n > 1 ? (size_t)(recs[1].out_off - recs[0].out_off) : 0, width = olen(recs[0]);
   for (uint32_t i = 1; i < n && pitched; i++)
@@ -338,14 +346,18 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
   hipStream_t s = e->stream;
   const bool dev_ptrs = flags & ATLS_FLAG_DEVICE_PTRS;
   const bool dev_recs = flags & ATLS_FLAG_DEVICE_RECS;
-  const bool lazy = (flags & ATLS_FLAG_LAZY_JOIN) && (flags & ATLS_FLAG_NO_SYNC) && dev_ptrs;
-  if (!lazy && join_pending(e)) return ATLS_INTERNAL_ERROR;  // a batch without the flag starts after all
-  if (!dev_ptrs && dev_recs) return ATLS_ILLEGAL_PARAMETER;  // host buffers need host-visible descriptors
-
   // No tags array: every record must carry its tag in the wire record (ATLS_MODE_WIRE). The
   // kernels then get the engine's scratch array, so a device-resident non-WIRE descriptor cannot
   // fault (it seals into scratch, or fails authentication on open).
   const bool no_tags = open ? !tags_in : !tags_out;
+  // A lazy batch leaves its side kernel running into the next batch, so it may use no engine buffer
+  // that the next batch rewrites or reallocates: the descriptors must be the caller's (DEVICE_RECS,
+  // not the engine's staging copy) and so must the tags (not the engine's scratch array). Any other
+  // batch joins the side kernels of earlier lazy batches first.
+  const bool lazy = (flags & ATLS_FLAG_LAZY_JOIN) && (flags & ATLS_FLAG_NO_SYNC) && dev_ptrs && dev_recs && !no_tags;
+  if (!lazy && join_pending(e)) return ATLS_INTERNAL_ERROR;  // a batch without the flag starts after all
+  if (!dev_ptrs && dev_recs) return ATLS_ILLEGAL_PARAMETER;  // host buffers need host-visible descriptors
+
   if (no_tags && !e->tags.reserve(16 * (size_t)n)) return ATLS_INTERNAL_ERROR;
   const atls_rec* d_recs = recs;
   if (!dev_recs) {
@@ -379,9 +391,13 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     // groups' 128-B runs of 8 records 16 KiB apart touch many host pages at once, where a copy engine
     // streams.
     if (e->zero_copy == 1) {
-      const void* zi = in_end ? host_alias(in, in_end) : e->in.p;
-      void* zo = out_end ? host_alias(out, out_end) : e->out.p;
-      const void* za = aux_end ? host_alias(aux, aux_end) : e->aux.p;
+      // a buffer the batch does not touch (extent 0, e.g. aux in TLS / WIRE batches) gets a placeholder the
+      // kernels never dereference: the engine's error word, which always exists (the engine's
+      // staging buffers are null on a fresh engine, which made the first call fall back to staging)
+      void* ph = e->err.p;
+      const void* zi = in_end ? host_alias(in, in_end) : ph;
+      void* zo = out_end ? host_alias(out, out_end) : ph;
+      const void* za = aux_end ? host_alias(aux, aux_end) : ph;
       const void* zt = no_tags ? e->tags.p : host_alias(open ? (const void*)tags_in : (const void*)tags_out, 16 * (size_t)n);
       void* zr = open ? host_alias(res, sizeof(atls_open_result) * (size_t)n) : (void*)res;
       if (zi && zo && za && zt && (zr || !open)) {
@@ -533,13 +549,20 @@ int install_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t 
     grown.p = nullptr;
     grown.cap = 0;
   }
-  if (!e->keys_stage.reserve(sizeof(atls_key) * (size_t)std::max<uint32_t>(n, 1))) return ATLS_INTERNAL_ERROR;
-  if (n && hipMemcpyAsync(e->keys_stage.p, keys, sizeof(atls_key) * (size_t)n, hipMemcpyHostToDevice, e->stream) !=
-               hipSuccess)
+  // A few keys (a connection's new key, the single call's cache miss) travel in the key-setup kernel's
+  // arguments: no staging copy and no host wait -- the kernel is ordered before every later batch by the
+  // engine stream, and the other streams start from events recorded on it. More keys are staged by one
+  // copy, and the call waits for the kernel (the caller's host array is read by that copy).
+  const bool inl = n <= (uint32_t)atls_key_setup_inline_max();
+  if (!inl) {
+    if (!e->keys_stage.reserve(sizeof(atls_key) * (size_t)n)) return ATLS_INTERNAL_ERROR;
+    if (hipMemcpyAsync(e->keys_stage.p, keys, sizeof(atls_key) * (size_t)n, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+      return ATLS_INTERNAL_ERROR;
+  }
+  if (atls_launch_key_setup(inl ? nullptr : (const atls_key*)e->keys_stage.p, keys, n, (atls::KeySched*)e->ks.p + first,
+                            e->stream))
     return ATLS_INTERNAL_ERROR;
-  if (atls_launch_key_setup((const atls_key*)e->keys_stage.p, n, (atls::KeySched*)e->ks.p + first, e->stream))
-    return ATLS_INTERNAL_ERROR;
-  if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  if (!inl && hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
   if (replace) e->keys.clear();
   if (e->keys.size() < total) e->keys.resize(total);
   std::copy(keys, keys + n, e->keys.begin() + first);
@@ -782,6 +805,9 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
     src = (const uint8_t*)e->in.p;
   }
   const uint32_t done_val = ++c->calls;
+  // the flag word holds anything after a (re)allocation of the block: set it to a value other than
+  // done_val, so only this launch's store ends the spin
+  __atomic_store_n((uint32_t*)(h + done_at), done_val - 1u, __ATOMIC_RELEASE);
   rc = launch_records(e, open, (const atls_rec*)(src + rec_at), 1, src, src, hd, hd + tag_at, src + tag_at,
                       (atls_open_result*)(hd + res_at), s, (uint32_t*)(hd + done_at), done_val);
   if (rc) return rc;
@@ -1059,11 +1085,23 @@ int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_
 
 }  // extern "C"
 
+// Debug: copy key slot `slot`'s device key schedule (atls_dev.h KeySched, 3,648 B) to host, for the tests
+// of the key-setup kernel against a host model (tests/test_gpu_keysetup.py). Returns its size or -1.
+extern "C" int atls_debug_key_sched(atls_engine* e, uint32_t slot, void* out, size_t cap) {
+  if (!e || !out || cap < sizeof(atls::KeySched)) return -1;
+  std::lock_guard<std::mutex> lk(e->mu);
+  if (slot >= e->n_slots || !set_dev(e) || hipStreamSynchronize(e->stream) != hipSuccess) return -1;
+  if (hipMemcpy(out, (const atls::KeySched*)e->ks.p + slot, sizeof(atls::KeySched), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return (int)sizeof(atls::KeySched);
+}
+
 // Debug: copy the last batch plan (PlanHdr words, then the first n_idx record indices) to host.
 extern "C" int atls_debug_plan(atls_engine* e, uint32_t* out, uint32_t n_idx) {
-  if (!e || !e->ps[e->last_par].plan.p) return -1;
-  std::lock_guard<std::mutex> lk(e->mu);
+  if (!e) return -1;
+  std::lock_guard<std::mutex> lk(e->mu);  // before reading last_par / the plan set
   const auto& q = e->ps[e->last_par];
+  if (!q.plan.p) return -1;
   if (!set_dev(e) || join_pending(e) || hipStreamSynchronize(e->stream) != hipSuccess) return -1;
   if (hipMemcpy(out, q.plan.p, sizeof(atls::PlanHdr), hipMemcpyDeviceToHost) != hipSuccess) return -1;
   if (n_idx && hipMemcpy(out + sizeof(atls::PlanHdr) / 4, q.idx.p, 4 * (size_t)n_idx, hipMemcpyDeviceToHost) != hipSuccess)

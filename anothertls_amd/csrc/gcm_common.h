@@ -97,7 +97,7 @@ __device__ __forceinline__ void ghash_mul_tab(uint32_t (&y)[4], uint32_t wb) {
       const v4u32 el = lds_u4(perm(lo4, wb, sel) + (2 * byte + 1) * 256);
       a0 = xor3(a0, eh.x, el.x); a1 = xor3(a1, eh.y, el.y); a2 = xor3(a2, eh.z, el.z); a3 = xor3(a3, eh.w, el.w);
     }
-    if (GROUP > 0 && ((i + 1) * 8) % GROUP == 0) __builtin_amdgcn_sched_barrier(0);
+    if (GROUP > 0 && ((i + 1) * 8) % (GROUP > 0 ? GROUP : 1) == 0) __builtin_amdgcn_sched_barrier(0);
   }
   y[0] = a0; y[1] = a1; y[2] = a2; y[3] = a3;
 }

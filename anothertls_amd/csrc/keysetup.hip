@@ -1,120 +1,242 @@
-// Device key setup: one thread per key slot (a connection's write key). Everything the
-// record kernels need per key is computed here once, instead of per record as the
-// reference does (gcm.rs:52-56 re-expands the key and recomputes H on every call):
-//   * AES round keys (crypto/aes/cipher.rs:216-249) as raw words for the T-table rounds;
+// Device key setup: one wavefront per key slot (a connection's write key). Everything the record
+// kernels need per key is computed here once, instead of per record as the reference does
+// (gcm.rs:52-56 re-expands the key and recomputes H on every call):
+//   * AES round keys (crypto/aes/cipher.rs:216-249) as raw words for the T-table rounds, and their rotl16;
 //   * H = E_K(0^128) (gcm.rs:56), H^1..H^64 (lane-combine multipliers), and
-//     x^(4p)*H^64 and x^(4p)*H^32 for p = 0..31 (seeds of the per-record 4-bit GHASH tables);
-//   * ChaCha20 key words (chacha20/cipher.rs:29-31).
+//     x^(4p)*H^64 and x^(4p)*H^(8<<t), t = 0..2, for p = 0..31 (seeds of the 4-bit GHASH tables);
+//   * ChaCha20 key words (chacha20/cipher.rs:29-31) and the static IV (key_schedule.rs:34).
 // Also builds the 256-entry AES T-table T0 used (replicated per LDS bank) by gcm.hip.
+//
+// Round 4: the first version ran one serial thread per key -- a private byte array AES
+// and 64 + 128 bit-serial products -- and took 0.459 ms for C2's 4,096 keys. Now a wave owns a key:
+//   * the key expansion and E_K(0) are wave-uniform T-table work on an LDS copy of T0 (unrolled per key
+//     size, so the round keys stay in registers);
+//   * H^1..H^64 come from a 6-level doubling scan -- at level k lanes [2^k, 2^(k+1)) multiply the
+//     power 2^k lanes below by H^(2^k), one factor for the whole wave -- each product by a 4-bit table of
+//     that factor built in the wave's LDS (gcm_common.h ghash_table_entries / ghash_mul_tab, the record
+//     kernels' own GHASH machinery: 32 lookups per product instead of a 128-step bit-serial loop);
+//   * every table seed x^k * Y is one shift and one reduction (gf_mulxk below), so the 32 seeds of a table
+//     and the 128 record-table seeds are computed by all lanes at once.
 #include "aes_sbox.h"
-#include "atls_dev.h"
+#include "gcm_common.h"
 
 namespace atls {
 
 // T0[x] = {2S, S, S, 3S} little-endian: MixColumns column of S[x] entering at row 0.
-__global__ void build_t0_kernel(uint32_t* __restrict__ t0) {
-  int x = threadIdx.x;
-  uint8_t s = kSbox[x], s2 = xtime(s), s3 = (uint8_t)(s2 ^ s);
-  t0[x] = (uint32_t)s2 | ((uint32_t)s << 8) | ((uint32_t)s << 16) | ((uint32_t)s3 << 24);
+__device__ __forceinline__ uint32_t t0_entry(int x) {
+  const uint8_t s = kSbox[x], s2 = xtime(s), s3 = (uint8_t)(s2 ^ s);
+  return (uint32_t)s2 | ((uint32_t)s << 8) | ((uint32_t)s << 16) | ((uint32_t)s3 << 24);
 }
 
-// Byte-oriented AES block encryption for setup only (one block per key: H).
-__device__ void aes_encrypt_bytes(const uint8_t* ek, int nr, const uint8_t in[16], uint8_t out[16]) {
-  uint8_t s[16];
-  for (int i = 0; i < 16; i++) s[i] = in[i] ^ ek[i];
-  for (int r = 1; r <= nr; r++) {
-    uint8_t t[16];
-    for (int c = 0; c < 4; c++)
-      for (int row = 0; row < 4; row++) t[4 * c + row] = kSbox[s[4 * ((c + row) & 3) + row]];
-    if (r < nr) {
-      for (int c = 0; c < 4; c++) {
-        uint8_t a0 = t[4 * c], a1 = t[4 * c + 1], a2 = t[4 * c + 2], a3 = t[4 * c + 3];
-        uint8_t x = a0 ^ a1 ^ a2 ^ a3;
-        t[4 * c] = a0 ^ x ^ xtime(a0 ^ a1);
-        t[4 * c + 1] = a1 ^ x ^ xtime(a1 ^ a2);
-        t[4 * c + 2] = a2 ^ x ^ xtime(a2 ^ a3);
-        t[4 * c + 3] = a3 ^ x ^ xtime(a3 ^ a0);
-      }
-    }
-    for (int i = 0; i < 16; i++) s[i] = t[i] ^ ek[16 * r + i];
+__global__ void build_t0_kernel(uint32_t* __restrict__ t0) { t0[threadIdx.x] = t0_entry((int)threadIdx.x); }
+
+// v <- v * x^m in GF(2^128), be words (gf_mulx_be applied m times), 1 <= m <= 64, m may differ per lane.
+// With V the 128-bit number v0:v1:v2:v3 (the coefficient of x^i at bit 127 - i), V * x^m = (V >> m) plus
+// the m low bits pushed past x^127: moved to the top as S = V << (128 - m) they stand for s(x) with
+// V * x^m's overflow = s(x) * x^128 = s(x) * (1 + x + x^2 + x^7) (the 0xE1 of gf_mulx_be), i.e.
+// S ^ S >> 1 ^ S >> 2 ^ S >> 7 -- no second reduction, deg s + 7 < 128.
+__host__ __device__ inline void gf_mulxk64(uint32_t (&v)[4], uint32_t m) {
+  const uint64_t hi = ((uint64_t)v[0] << 32) | v[1], lo = ((uint64_t)v[2] << 32) | v[3];
+  uint64_t rhi, rlo, s;
+  if (m >= 64) {
+    rhi = 0;
+    rlo = hi;
+    s = lo;
+  } else {
+    rhi = hi >> m;
+    rlo = (lo >> m) | (hi << (64 - m));
+    s = lo << (64 - m);
   }
-  for (int i = 0; i < 16; i++) out[i] = s[i];
+  rhi ^= s ^ (s >> 1) ^ (s >> 2) ^ (s >> 7);
+  rlo ^= (s << 63) ^ (s << 62) ^ (s << 57);
+  v[0] = (uint32_t)(rhi >> 32);
+  v[1] = (uint32_t)rhi;
+  v[2] = (uint32_t)(rlo >> 32);
+  v[3] = (uint32_t)rlo;
 }
 
-__global__ void key_setup_kernel(const atls_key* __restrict__ keys, uint32_t n, KeySched* __restrict__ ks) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const atls_key k = keys[i];
-  KeySched* o = &ks[i];
-  o->suite = k.suite;
-  o->key_len = k.key_len;
-  o->nr = 0;
-  o->valid = 0;
-  for (int w = 0; w < 3; w++)
-    o->siv[w] = (uint32_t)k.static_iv[4 * w] | ((uint32_t)k.static_iv[4 * w + 1] << 8) |
-                ((uint32_t)k.static_iv[4 * w + 2] << 16) | ((uint32_t)k.static_iv[4 * w + 3] << 24);
-  o->siv[3] = 0;
-  for (int w = 0; w < 8; w++)
-    o->kw[w] = (uint32_t)k.key[4 * w] | ((uint32_t)k.key[4 * w + 1] << 8) | ((uint32_t)k.key[4 * w + 2] << 16) |
-               ((uint32_t)k.key[4 * w + 3] << 24);
-  if (k.suite == kSuiteChacha) {
-    o->valid = (k.key_len == 32) ? 1u : 0u;
+// v <- v * x^m, 0 <= m <= 127.
+__host__ __device__ inline void gf_mulxk(uint32_t (&v)[4], uint32_t m) {
+  if (m > 64) {
+    gf_mulxk64(v, 64);
+    m -= 64;
+  }
+  if (m) gf_mulxk64(v, m);
+}
+
+// The wave's 4-bit table of the wave-uniform factor y (be words) at LDS byte address wb: lane l writes
+// entries 8 (l & 1) .. +7 of position l >> 1 from the seed x^(4p) * y (gcm_common.h layout).
+__device__ __forceinline__ void table_of(uint32_t wb, const uint32_t (&y)[4], int lane) {
+  const int p = lane >> 1;
+  uint32_t seed[4] = {y[0], y[1], y[2], y[3]};
+  gf_mulxk(seed, 4u * (uint32_t)p);
+  ghash_table_entries<8>(wb, seed, p, (lane & 1) * 8);
+}
+
+// x <- x * (the table's factor), be words in and out.
+__device__ __forceinline__ void table_mul(uint32_t (&x)[4], uint32_t wb) {
+  uint32_t r[4] = {bswap32(x[0]), bswap32(x[1]), bswap32(x[2]), bswap32(x[3])};
+  ghash_mul_tab(r, wb);
+  for (int w = 0; w < 4; w++) x[w] = bswap32(r[w]);
+}
+
+__device__ __forceinline__ uint32_t sbox_lds(const uint32_t* t0, uint32_t x) { return (t0[x & 255u] >> 8) & 0xffu; }
+__device__ __forceinline__ uint32_t sub_word(const uint32_t* t0, uint32_t w) {
+  return sbox_lds(t0, w) | (sbox_lds(t0, w >> 8) << 8) | (sbox_lds(t0, w >> 16) << 16) | (sbox_lds(t0, w >> 24) << 24);
+}
+
+// FIPS-197 key expansion (crypto/aes/cipher.rs:216-249) in raw little-endian words (word w = bytes 4w..4w+3
+// of the expanded key), unrolled per key size so every round key lives in a register; then H = E_K(0^128)
+// (gcm.rs:56) by T-table rounds (wave-uniform indices: LDS broadcasts). h_raw: H as raw words.
+template <int NK>
+__device__ __forceinline__ void expand_and_h(const uint32_t (&kw)[8], const uint32_t* t0, uint32_t (&rk)[60],
+                                             uint32_t (&h_raw)[4]) {
+  constexpr int NR = NK + 6, NW = 4 * (NR + 1);
+  constexpr uint32_t kRcon[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1B, 0x36};
+#pragma unroll
+  for (int w = 0; w < 60; w++) rk[w] = w < NK ? kw[w] : 0u;
+#pragma unroll
+  for (int w = NK; w < NW; w++) {
+    uint32_t t = rk[w - 1];
+    if (w % NK == 0) t = sub_word(t0, rotl32(t, 24)) ^ kRcon[w / NK - 1];  // RotWord = bytes (1,2,3,0)
+    else if (NK > 6 && w % NK == 4) t = sub_word(t0, t);
+    rk[w] = rk[w - NK] ^ t;
+  }
+  uint32_t s0 = rk[0], s1 = rk[1], s2 = rk[2], s3 = rk[3];  // AddRoundKey of the zero block
+#pragma unroll
+  for (int r = 1; r < NR; r++) {
+    const uint32_t a0 = t0[s0 & 255u] ^ rotl32(t0[(s1 >> 8) & 255u], 8) ^ rotl32(t0[(s2 >> 16) & 255u], 16) ^
+                        rotl32(t0[s3 >> 24], 24) ^ rk[4 * r];
+    const uint32_t a1 = t0[s1 & 255u] ^ rotl32(t0[(s2 >> 8) & 255u], 8) ^ rotl32(t0[(s3 >> 16) & 255u], 16) ^
+                        rotl32(t0[s0 >> 24], 24) ^ rk[4 * r + 1];
+    const uint32_t a2 = t0[s2 & 255u] ^ rotl32(t0[(s3 >> 8) & 255u], 8) ^ rotl32(t0[(s0 >> 16) & 255u], 16) ^
+                        rotl32(t0[s1 >> 24], 24) ^ rk[4 * r + 2];
+    const uint32_t a3 = t0[s3 & 255u] ^ rotl32(t0[(s0 >> 8) & 255u], 8) ^ rotl32(t0[(s1 >> 16) & 255u], 16) ^
+                        rotl32(t0[s2 >> 24], 24) ^ rk[4 * r + 3];
+    s0 = a0; s1 = a1; s2 = a2; s3 = a3;
+  }
+  const uint32_t st[4] = {s0, s1, s2, s3};
+#pragma unroll
+  for (int c = 0; c < 4; c++)  // SubBytes + ShiftRows (row r from column c + r) + the last round key
+    h_raw[c] = (sbox_lds(t0, st[c]) | (sbox_lds(t0, st[(c + 1) & 3] >> 8) << 8) |
+                (sbox_lds(t0, st[(c + 2) & 3] >> 16) << 16) | (sbox_lds(t0, st[(c + 3) & 3] >> 24) << 24)) ^
+               rk[4 * NR + c];
+}
+
+// Up to kInlineKeys keys travel in the kernel arguments (a connection's new key: no staging copy).
+constexpr int kInlineKeys = 4;
+constexpr int kSetupWaves = 4;                 // keys per workgroup
+constexpr uint32_t kSetupTab = 8192;           // one 4-bit table per wave
+constexpr uint32_t kSetupT0 = kSetupWaves * kSetupTab;
+struct KeySetupArgs {
+  const atls_key* keys;  // device array, or nullptr: the keys are in `inl`
+  uint32_t n;
+  KeySched* ks;
+  uint32_t inl[kInlineKeys][16];
+};
+static_assert(sizeof(atls_key) == 64, "atls_key is 16 words");
+
+__global__ __launch_bounds__(64 * kSetupWaves) void key_setup_kernel(KeySetupArgs A) {
+  extern __shared__ __attribute__((aligned(256))) uint32_t smem[];
+  uint32_t* t0 = smem + kSetupT0 / 4;
+  t0[threadIdx.x] = t0_entry((int)threadIdx.x);
+  __syncthreads();
+  const int wave = (int)uni(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const uint32_t i = blockIdx.x * kSetupWaves + (uint32_t)wave;
+  if (i >= A.n) return;
+  // the key's 16 words (atls_key: suite | key_len | iv_len, key[32], static_iv[12], reserved)
+  uint32_t k[16];
+  if (A.keys) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) k[q] = cptr(reinterpret_cast<const uint32_t*>(A.keys + i))[q];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 16; q++) k[q] = i == 0 ? A.inl[0][q] : i == 1 ? A.inl[1][q] : i == 2 ? A.inl[2][q] : A.inl[3][q];
+  }
+  const uint32_t suite = k[0] & 0xffffu, key_len = (k[0] >> 16) & 0xffu;
+  KeySched* o = A.ks + i;
+  uint32_t kw[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) kw[q] = k[1 + q];
+  // ChaCha20 key words and the static IV for every slot (the GCM kernels read siv too): word q of each
+  // from lane q (selects, no indexed register access)
+  {
+    uint32_t kq = 0, sq = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) kq = lane == q ? kw[q] : kq;
+#pragma unroll
+    for (int q = 0; q < 3; q++) sq = lane == q ? k[9 + q] : sq;
+    if (lane < 8) o->kw[lane] = kq;
+    if (lane < 4) o->siv[lane] = sq;
+  }
+  const bool aes = (suite == kSuiteAes128 || suite == kSuiteAes256) && (key_len == 16 || key_len == 24 || key_len == 32);
+  if (!aes) {
+    if (lane == 0) {
+      o->suite = suite;
+      o->nr = 0;
+      o->key_len = key_len;
+      o->valid = (suite == kSuiteChacha && key_len == 32) ? 1u : 0u;
+    }
     return;
   }
-  if (k.suite != kSuiteAes128 && k.suite != kSuiteAes256) return;
-  if (k.key_len != 16 && k.key_len != 24 && k.key_len != 32) return;  // gcm.rs:49 Blocksize::new
-  // FIPS-197 key expansion, crypto/aes/cipher.rs:216-249.
-  const int nk = k.key_len / 4, nr = nk + 6;
-  uint8_t ek[240];
-  const uint8_t rcon[10] = {0x01, 0x02, 0x04, 0x08, 0x10, 0x20, 0x40, 0x80, 0x1B, 0x36};
-  for (int j = 0; j < 4 * nk; j++) ek[j] = k.key[j];
-  for (int w = nk; w < 4 * (nr + 1); w++) {
-    uint8_t t[4] = {ek[4 * (w - 1)], ek[4 * (w - 1) + 1], ek[4 * (w - 1) + 2], ek[4 * (w - 1) + 3]};
-    if (w % nk == 0) {
-      uint8_t t0 = t[0];
-      t[0] = kSbox[t[1]] ^ rcon[w / nk - 1];
-      t[1] = kSbox[t[2]];
-      t[2] = kSbox[t[3]];
-      t[3] = kSbox[t0];
-    } else if (nk > 6 && w % nk == 4) {
-      for (int b = 0; b < 4; b++) t[b] = kSbox[t[b]];
-    }
-    for (int b = 0; b < 4; b++) ek[4 * w + b] = ek[4 * (w - nk) + b] ^ t[b];
-  }
-  for (int w = 0; w < 60; w++)
-    o->rk[w] = w < 4 * (nr + 1) ? ((uint32_t)ek[4 * w] | ((uint32_t)ek[4 * w + 1] << 8) |
-                                   ((uint32_t)ek[4 * w + 2] << 16) | ((uint32_t)ek[4 * w + 3] << 24))
-                                : 0u;
-  for (int w = 0; w < 60; w++) o->rkr[w] = (o->rk[w] << 16) | (o->rk[w] >> 16);
-  o->nr = (uint32_t)nr;
-  // H = E_K(0) (gcm.rs:56) and its powers.
-  uint8_t zero[16] = {0}, hb[16];
-  aes_encrypt_bytes(ek, nr, zero, hb);
-  uint32_t h[4];
-  for (int w = 0; w < 4; w++)
-    h[w] = ((uint32_t)hb[4 * w] << 24) | ((uint32_t)hb[4 * w + 1] << 16) | ((uint32_t)hb[4 * w + 2] << 8) | hb[4 * w + 3];
-  for (int w = 0; w < 4; w++) o->h_be[w] = h[w];
-  uint32_t p[4] = {h[0], h[1], h[2], h[3]};
-  for (int e = 0; e < 64; e++) {
-    for (int w = 0; w < 4; w++) o->hpow_be[e][w] = p[w];
-    uint32_t q[4];
-    gf_mul_be(p, h, q);
-    for (int w = 0; w < 4; w++) p[w] = q[w];
-  }
-  // p4[j] = x^(4j) * H^64; p4g[t][j] = x^(4j) * H^(8 << t) (records processed in lane groups)
-  uint32_t v[4] = {o->hpow_be[63][0], o->hpow_be[63][1], o->hpow_be[63][2], o->hpow_be[63][3]};
-  for (int j = 0; j < 32; j++) {
-    for (int w = 0; w < 4; w++) o->p4_be[j][w] = v[w];
-    gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v);
-  }
-  for (int t = 0; t < 3; t++) {
-    for (int w = 0; w < 4; w++) v[w] = o->hpow_be[(8 << t) - 1][w];
-    for (int j = 0; j < 32; j++) {
-      for (int w = 0; w < 4; w++) o->p4g_be[t][j][w] = v[w];
-      gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v); gf_mulx_be(v);
+  uint32_t rk[60], h[4];
+  if (key_len == 16) expand_and_h<4>(kw, t0, rk, h);
+  else if (key_len == 24) expand_and_h<6>(kw, t0, rk, h);
+  else expand_and_h<8>(kw, t0, rk, h);
+  const uint32_t nr = key_len / 4 + 6;
+  {  // round key w from lane w (one coalesced store each for rk and rkr)
+    uint32_t mine = 0;
+#pragma unroll
+    for (int w = 0; w < 60; w++) mine = lane == w ? rk[w] : mine;
+    if (lane < 60) {
+      o->rk[lane] = mine;
+      o->rkr[lane] = rot16(mine);
     }
   }
-  o->valid = 1;
+  uint32_t hb[4];
+#pragma unroll
+  for (int w = 0; w < 4; w++) hb[w] = bswap32(h[w]);
+  if (lane < 4) o->h_be[lane] = lane == 0 ? hb[0] : lane == 1 ? hb[1] : lane == 2 ? hb[2] : hb[3];
+  // H^(lane+1): doubling scan, each level's products by a table of the level's one factor H^(2^k)
+  const uint32_t wb = (uint32_t)wave * kSetupTab;
+  uint32_t P[4] = {hb[0], hb[1], hb[2], hb[3]};
+#pragma unroll 1
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) y[w] = (uint32_t)__builtin_amdgcn_readlane((int)P[w], d - 1);
+    wave_lds_sync();  // the previous level's table reads are done before the table is rebuilt
+    table_of(wb, y, lane);
+    wave_lds_sync();
+    uint32_t x[4];
+    const int src = lane >= d ? lane - d : lane;
+#pragma unroll
+    for (int w = 0; w < 4; w++) x[w] = (uint32_t)__shfl((int)P[w], src, 64);
+    table_mul(x, wb);
+    if (lane >= d && lane < 2 * d) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) P[w] = x[w];
+    }
+  }
+  *reinterpret_cast<uint4*>(o->hpow_be[lane]) = make_uint4(P[0], P[1], P[2], P[3]);
+  // record-table seeds: x^(4p) * H^64 (p4_be) and x^(4p) * H^(8 << t) (p4g_be[t]), 128 in all, 2 per lane
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+    const int idx = lane + 64 * s, set = idx >> 5, p = idx & 31;
+    const int from = set == 0 ? 63 : (8 << (set - 1)) - 1;  // lane holding H^64, H^8, H^16, H^32
+    uint32_t v[4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) v[w] = (uint32_t)__shfl((int)P[w], from, 64);
+    gf_mulxk(v, 4u * (uint32_t)p);
+    uint32_t* dst = set == 0 ? o->p4_be[p] : o->p4g_be[set - 1][p];
+    *reinterpret_cast<uint4*>(dst) = make_uint4(v[0], v[1], v[2], v[3]);
+  }
+  if (lane == 0) {
+    o->suite = suite;
+    o->nr = nr;
+    o->key_len = key_len;
+    o->valid = 1u;
+  }
 }
 
 }  // namespace atls
@@ -124,9 +246,22 @@ extern "C" int atls_launch_build_t0(uint32_t* t0, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
 
-extern "C" int atls_launch_key_setup(const atls_key* keys, uint32_t n, void* ks, hipStream_t s) {
+// keys: a device array of n keys, or (n <= atls_key_setup_inline_max()) nullptr with host_keys, whose
+// contents then travel in the kernel arguments (no copy, nothing to wait for before the call returns).
+extern "C" int atls_key_setup_inline_max(void) { return atls::kInlineKeys; }
+extern "C" int atls_launch_key_setup(const atls_key* keys, const atls_key* host_keys, uint32_t n, void* ks,
+                                     hipStream_t s) {
   if (n == 0) return 0;
-  hipLaunchKernelGGL(atls::key_setup_kernel, dim3((n + 63) / 64), dim3(64), 0, s, keys, n,
-                     (atls::KeySched*)ks);
+  atls::KeySetupArgs A{};
+  A.keys = keys;
+  A.n = n;
+  A.ks = (atls::KeySched*)ks;
+  if (!keys) {
+    if (!host_keys || n > (uint32_t)atls::kInlineKeys) return ATLS_INTERNAL_ERROR;
+    __builtin_memcpy(A.inl, host_keys, sizeof(atls_key) * n);
+  }
+  const uint32_t blocks = (n + atls::kSetupWaves - 1) / atls::kSetupWaves;
+  hipLaunchKernelGGL(atls::key_setup_kernel, dim3(blocks), dim3(64 * atls::kSetupWaves),
+                     atls::kSetupT0 + 1024, s, A);
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }

@@ -117,6 +117,21 @@ def records_per_rank(name):
     return n_full // 8 if name in EIGHT_GPU_CONFIGS else n_full
 
 
+def capped(b, cap):
+    """The batch b with every content length cut to at most `cap` bytes and the records re-packed
+    (same records, keys, slots and sequence numbers). For CPU rehearsals of whole-config exchanges
+    (bench.py --dry-run): C4's 1 Mi records at 16 KiB are 34 GB of buffers, at 64 B 150 MB."""
+    recs = b["recs"].copy()
+    lens = np.minimum(recs["len"].astype(np.uint64), np.uint64(cap))
+    in_sz, out_sz = _round16(lens), _round16(lens + np.uint64(1))
+    n = len(recs)
+    recs["len"] = lens.astype(np.uint32)
+    recs["in_off"] = np.concatenate([[0], np.cumsum(in_sz)[:-1]]).astype(np.uint64) if n else []
+    recs["out_off"] = np.concatenate([[0], np.cumsum(out_sz)[:-1]]).astype(np.uint64) if n else []
+    return dict(b, recs=recs, in_bytes=int(in_sz.sum()) if n else 0, out_bytes=int(out_sz.sum()) if n else 0,
+                payload=int(lens.sum() + n))
+
+
 def shard_batch(name, rank, n=None, n_keys=None):
     """Rank `rank`'s shard: records rank*n .. rank*n+n-1 of the config's record stream (key slots,
     sequence numbers and lengths as in the unsharded batch). n defaults to records_per_rank()."""

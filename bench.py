@@ -68,6 +68,11 @@ def parse():
     p.add_argument("--no-open", action="store_true", help="skip the open (decrypt) half of the measurement")
     p.add_argument("--no-lazy-join", action="store_true",
                    help="join a mixed batch's side kernel at the end of every step (A/B of ATLS_FLAG_LAZY_JOIN)")
+    p.add_argument("--no-configs", action="store_true",
+                   help="skip the other BASELINE configs (C3, C4 shard, C5 shard) timed after the headline one")
+    p.add_argument("--config-steps", type=int, default=10, help="timed steps of each of those configs")
+    p.add_argument("--dry-run-cap", type=int, default=64,
+                   help="--dry-run: content bytes per record of the whole-batch exchange rehearsal")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU only (gloo): the launcher, rendezvous, timing and JSON line with a stub sealer "
                         "instead of the engine (tests of the N > 1 plumbing)")
@@ -124,35 +129,54 @@ def cpu_baseline(batch, inbuf_host, budget_s, threads):
                        f"{d1} records ({p1} B) in {t1:.1f} s")
 
 
-def sharded_exchange(args, eng, dev, d_in, d_aux, d_ref_out, d_ref_tags, reps=3):
-    """Rank 0's batch (its shard of the config) sealed by all ranks through dist.seal_sharded
-    (byte-balanced split, RCCL point-to-point scatter / gather, each rank's engine on its range).
-    Returns (rank 0) GiB/s of AEAD payload for scatter + seal + gather, max time over ranks, and
-    whether the gathered bytes equal rank 0's single-GPU result."""
-    import anothertls_amd as atls
-    from anothertls_amd import dist, workload
+def whole_batch(args, world):
+    """The config's WHOLE record batch (BASELINE's stated size: C4 1 Mi records, C5 256 Ki, C2 / C3 64 Ki),
+    or --records x world records when --records overrides the per-GPU count."""
+    from anothertls_amd import workload
 
-    b0 = workload.shard_batch(args.config, 0, n=args.records, n_keys=args.key_slots)  # same on every rank
+    n = args.records * world if args.records else None
+    return workload.config_batch(args.config, n=n, n_keys=args.key_slots)
+
+
+def sharded_exchange(batch, seal, make_input, zeros, sync, device=None, reps=3):
+    """A batch that arrives whole at rank 0 (C4 is stated as 1 Mi records sharded across 8
+    GPUs) sealed by every rank through dist.seal_sharded: byte-balanced split (atls_partition), RCCL
+    point-to-point scatter of the input and output ranges, each rank's engine on its range, gather of
+    the sealed ranges and tags back. Rank 0 first seals the whole batch alone, the reference the
+    gathered bytes must equal. Returns (rank 0) GiB/s of AEAD payload for scatter + seal + gather,
+    max time over ranks; None on the other ranks."""
+    from anothertls_amd import dist
+
+    recs = batch["recs"]
+    n = len(recs)
     rank = dist.env_ranks()[0]
-    out = tags = None
+    inp = out = tags = ref_out = ref_tags = None
     if rank == 0:
-        out = torch.zeros_like(d_ref_out)
-        tags = torch.zeros_like(d_ref_tags)
-
-    def seal(recs, inp, o, t):
-        eng.seal_batch(recs, inp, d_aux, o, t, flags=atls.FLAG_DEVICE_PTRS)  # synchronous
+        inp = make_input(batch["in_bytes"] + 16)
+        ref_out, ref_tags = zeros(batch["out_bytes"] + 16), zeros(16 * n)
+        seal(recs, inp, ref_out, ref_tags)  # the whole batch on rank 0's GPU alone
+        out, tags = zeros(batch["out_bytes"] + 16), zeros(16 * n)
+    sync()
 
     def run():
-        dist.seal_sharded(seal, b0["recs"], d_in, out, tags, device=dev)
+        dist.seal_sharded(seal, recs, inp, out, tags, device=device)
 
     run()  # warm-up: communicators, staging
-    wall = dist.timed_steps(run, reps, 0, lambda: torch.cuda.synchronize(dev), dev)
+    wall = dist.timed_steps(run, reps, 0, sync, device)
     if rank != 0:
         return None
-    match = bool(torch.equal(out, d_ref_out) and torch.equal(tags, d_ref_tags))
-    return {"GiBps": round(b0["payload"] * reps / wall / 2**30, 3), "ms": round(wall / reps * 1e3, 3),
-            "matches_single_gpu": match, "records": len(b0["recs"]),
-            "path": "dist.seal_sharded: atls_partition byte split, torch.distributed P2P (RCCL over xGMI)"}
+    import torch
+
+    match = bool(torch.equal(out, ref_out) and torch.equal(tags, ref_tags))
+    world = dist.world_size()
+    import anothertls_amd as atls
+
+    first = atls.partition(recs, world)
+    return {"GiBps": round(batch["payload"] * reps / wall / 2**30, 3), "ms": round(wall / reps * 1e3, 3),
+            "matches_single_gpu": match, "records": n, "payload_bytes": batch["payload"],
+            "records_per_rank": [int(first[r + 1] - first[r]) for r in range(world)],
+            "path": "rank 0 holds the whole batch; dist.seal_sharded: atls_partition byte split, torch.distributed "
+                    "P2P (RCCL over xGMI) scatter / gather, every rank's engine on its range"}
 
 
 C1 = "c1_server_https_loopback_1MiB"
@@ -220,10 +244,34 @@ def run_c1(args):
     print(json.dumps(result), flush=True)
 
 
+def _stub_sealer():
+    """--dry-run's stand-in for the engine on CPU tensors: content XOR 0x5A and the content type out,
+    tag = (seq, len) -- deterministic per record whatever the offsets, so a sharded seal must equal the
+    whole batch's."""
+
+    def seal(recs, inp, out, tags):
+        L = recs["len"].astype(np.int64)
+        tot = int(L.sum())
+        a, o = inp.numpy(), out.numpy()
+        if tot:
+            start = np.repeat(np.cumsum(L) - L, L)
+            j = np.arange(tot, dtype=np.int64) - start
+            o[np.repeat(recs["out_off"].astype(np.int64), L) + j] = a[np.repeat(recs["in_off"].astype(np.int64), L) + j] ^ 0x5A
+        o[recs["out_off"].astype(np.int64) + L] = recs["content_type"]
+        t = np.zeros((len(recs), 2), np.uint64)
+        t[:, 0], t[:, 1] = recs["seq"], recs["len"]
+        tags.numpy()[:] = t.view(np.uint8).ravel()
+
+    return seal
+
+
 def run_dry(args):
     """--dry-run: this rank's part of an N-rank job on the CPU (gloo) with a stub sealer (a byte XOR
     over a small C2-shaped shard) in place of the engine -- the launcher, rendezvous, barrier +
-    max-over-ranks timing and the JSON line of the real run, without a GPU (tests/test_bench_launch.py)."""
+    max-over-ranks timing and the JSON line of the real run, without a GPU (tests/test_bench_launch.py).
+    For N > 1 also the whole-batch exchange of the real run (sharded_from_rank0) over the config's full
+    record list -- every record, slot and sequence number, contents cut to --dry-run-cap bytes so C4's
+    1 Mi records fit a CPU rehearsal."""
     from anothertls_amd import dist, workload
 
     rank, _, world = dist.env_ranks()
@@ -237,13 +285,24 @@ def run_dry(args):
 
     wall = dist.timed_steps(step, args.steps, args.warmup, lambda: None)
     ranks = dist.world_size()
+    line = {"metric": METRIC, "value": round(dist.whole_job_rate(batch["payload"], args.steps, wall, ranks), 3),
+            "unit": "GiB/s", "n_gpus": ranks, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+            "dry_run": True, "config": {"workload": args.config, "records_per_gpu": len(batch["recs"])}}
+    if ranks > 1 and not args.no_scatter:
+        import torch
+
+        whole = workload.capped(whole_batch(args, ranks), args.dry_run_cap)
+        sg = sharded_exchange(
+            whole, _stub_sealer(),
+            lambda nb: torch.from_numpy(np.random.default_rng(5).integers(0, 256, nb, dtype=np.uint8)),
+            lambda nb: torch.zeros(nb, dtype=torch.uint8), lambda: None, reps=1)
+        if rank == 0:
+            sg["dry_run_content_cap"] = args.dry_run_cap
+            line["sharded_from_rank0"] = sg
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": round(dist.whole_job_rate(batch["payload"], args.steps, wall, ranks), 3),
-                          "unit": "GiB/s", "n_gpus": ranks, "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-                          "dry_run": True, "config": {"workload": args.config, "records_per_gpu": len(batch["recs"])}}),
-              flush=True)
+        print(json.dumps(line), flush=True)
     dist.close()
 
 
@@ -255,6 +314,121 @@ def open_descs(recs):
     o["in_off"] = recs["out_off"]
     o["len"] = recs["len"] + 1
     return o
+
+
+# The BASELINE configs timed beside the headline one: C3 whole, the per-GPU shards of C4
+# and C5 (1/8 of their 8-GPU batches; at N GPUs every rank runs its own shard, so at N = 8 they are the
+# whole configs).
+EXTRA_CONFIGS = ("c3_chacha20poly1305_64Ki_x_1.5KiB", "c4_aes256gcm_1Mi_x_16KiB", "c5_mixed_256Ki_x_64B-16KiB")
+
+
+def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_slots=None, keep=False):
+    """This rank's shard of config `name`, device-resident: `steps` timed seals (barrier + sync on both
+    sides, max over ranks) with the kernels' interval from HIP events on the engine stream, then as many
+    opens of the sealed records with every status, length and (uniform configs) plaintext byte checked.
+    Returns the numbers (and with keep=True the batch and its device buffers)."""
+    import anothertls_amd as atls
+    from anothertls_amd import dist, workload
+
+    batch = workload.shard_batch(name, rank, n=records, n_keys=key_slots)
+    recs = batch["recs"]
+    n = len(recs)
+    eng.set_keys(batch["keys"])
+    g = torch.Generator(device=dev).manual_seed(workload.SEEDS["payload"] + rank)
+    d_in = torch.randint(0, 256, (batch["in_bytes"],), dtype=torch.uint8, device=dev, generator=g)
+    d_out = torch.empty(batch["out_bytes"], dtype=torch.uint8, device=dev)
+    d_tags = torch.empty(16 * n, dtype=torch.uint8, device=dev)
+    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+    d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
+    torch.cuda.synchronize(dev)
+    # LAZY_JOIN: a mixed batch's ChaCha20-Poly1305 kernel is not joined back at the end of each step,
+    # so the next step's plan and AES-GCM kernel start beside it (C5); no effect on one-suite batches
+    flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC | (atls.FLAG_LAZY_JOIN if lazy else 0)
+    stream = torch.cuda.ExternalStream(eng.stream, device=dev)
+    # raw device pointers: the buffers are resident and synchronized above, so no per-step wait
+    # on torch's stream is needed (Engine._after_torch)
+    p_recs, p_in, p_aux, p_out, p_tags = (t.data_ptr() for t in (d_recs, d_in, d_aux, d_out, d_tags))
+
+    def sync():
+        eng.sync()
+        torch.cuda.synchronize(dev)
+
+    # kernel time of the same steps from HIP events on the engine's stream
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    marks = {"n": 0}
+
+    def timed_step():
+        if marks["n"] == warmup:
+            eng.join()  # the interval holds exactly the timed steps' kernels
+            ev0.record(stream)
+        eng.seal_batch(p_recs, p_in, p_aux, p_out, p_tags, flags=flags, n=n)
+        marks["n"] += 1
+        if marks["n"] == warmup + steps:
+            eng.join()
+            ev1.record(stream)
+
+    wall = dist.timed_steps(timed_step, steps, warmup, sync, dev)
+    kern_ms = ev0.elapsed_time(ev1) / steps
+    payload = batch["payload"]  # sum of AEAD lengths (content + type byte)
+    alg_bytes = 2 * payload + 16 * n
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    m = {"batch": batch, "n": n, "wall": wall, "kern_ms": kern_ms, "payload": payload, "alg_bytes": alg_bytes,
+         "achieved": achieved, "value": dist.whole_job_rate(payload, steps, wall, world), "flags": flags,
+         "stream": stream, "sync": sync}
+
+    # ---- the decrypt half (Gcm::decrypt, gcm.rs:142-157, via record.rs:201-240) over the records
+    # just sealed: same records, same bytes per record (read L + 16-byte tag, write L) ----
+    orecs = open_descs(recs)
+    d_orecs = torch.from_numpy(orecs.view(np.uint8).copy()).to(dev)
+    d_pt = torch.zeros(batch["out_bytes"], dtype=torch.uint8, device=dev)
+    d_res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize(dev)
+    q_recs, q_pt, q_res = d_orecs.data_ptr(), d_pt.data_ptr(), d_res.data_ptr()
+    o0, o1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for i in range(warmup + steps):
+        if i == warmup:
+            eng.join()
+            o0.record(stream)
+        eng.open_batch(q_recs, p_out, p_aux, p_tags, q_pt, q_res, flags=flags, n=n)
+    eng.join()
+    o1.record(stream)
+    sync()
+    open_ms = o0.elapsed_time(o1) / steps
+    res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
+    ok = bool((res["status"] == 0).all() and (res["content_len"] == recs["len"]).all()
+              and (res["content_type"] == 23).all())
+    lens = recs["len"]
+    if ok and n > 1 and (lens == lens[0]).all() and (np.diff(recs["in_off"]) == recs["in_off"][1] - recs["in_off"][0]).all() \
+            and (np.diff(recs["out_off"]) == recs["out_off"][1] - recs["out_off"][0]).all():
+        # uniform records (C2-C4): every plaintext byte of every record against the sealed input
+        L, si, so = int(lens[0]), int(recs["in_off"][1] - recs["in_off"][0]), int(recs["out_off"][1] - recs["out_off"][0])
+        ok = bool(torch.equal(d_pt[: n * so].view(n, so)[:, :L], d_in[: n * si].view(n, si)[:, :L]))
+    open_ach = alg_bytes / (open_ms * 1e-3) / 1e9  # read L+1 ciphertext + 16 tag, write L+1 plaintext
+    m["open"] = {"GiBps": round(payload / (open_ms * 1e-3) / 2**30, 3), "kernel_ms": round(open_ms, 4),
+                 "achieved_GBps": round(open_ach, 1), "frac": round(open_ach / HBM_PEAK_GBPS, 4),
+                 "plaintext_and_status_ok": ok,
+                 "what": "open_batch over the sealed records (device-resident, same batch), HIP events on the "
+                         "engine stream over the timed steps"}
+    del d_orecs, d_pt, d_res
+    if keep:
+        m.update(d_in=d_in, d_out=d_out, d_tags=d_tags, d_aux=d_aux, d_recs=d_recs)
+    else:
+        del d_in, d_out, d_tags, d_recs
+        torch.cuda.empty_cache()
+    return m
+
+
+def config_summary(name, m, steps):
+    """One `configs` entry: seal and open GiB/s, kernel interval and HBM-roofline fraction."""
+    from anothertls_amd import workload
+
+    suite, _, clen = workload.CONFIGS[name]
+    return {"records_per_gpu": m["n"], "steps": steps, "GiBps": round(m["value"], 3),
+            "kernel_ms": round(m["kern_ms"], 4), "achieved_GBps": round(m["achieved"], 1),
+            "frac": round(m["achieved"] / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": m["alg_bytes"],
+            "suite": suite if isinstance(suite, str) else suite.name,
+            "aead_bytes_per_record": (clen + 1) if isinstance(clen, int) else "content U{64..16384}+1",
+            "open": {k: v for k, v in m["open"].items() if k != "what"}}
 
 
 def main():
@@ -288,94 +462,13 @@ def main():
     import anothertls_amd as atls
     from anothertls_amd import workload
 
-    # this rank's shard of the config's record stream (weak scaling: fixed records per GPU)
-    batch = workload.shard_batch(args.config, rank, n=args.records, n_keys=args.key_slots)
-    recs = batch["recs"]
-    n = len(recs)
     eng = atls.Engine(local)
-    eng.set_keys(batch["keys"])
-    g = torch.Generator(device=dev).manual_seed(workload.SEEDS["payload"] + rank)
-    d_in = torch.randint(0, 256, (batch["in_bytes"],), dtype=torch.uint8, device=dev, generator=g)
-    d_out = torch.empty(batch["out_bytes"], dtype=torch.uint8, device=dev)
-    d_tags = torch.empty(16 * n, dtype=torch.uint8, device=dev)
-    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
-    d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
-    torch.cuda.synchronize(dev)
-    # LAZY_JOIN: a mixed batch's ChaCha20-Poly1305 kernel is not joined back at the end of each step,
-    # so the next step's plan and AES-GCM kernel start beside it (C5); no effect on one-suite batches
-    flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC | (0 if args.no_lazy_join else atls.FLAG_LAZY_JOIN)
-    stream = torch.cuda.ExternalStream(eng.stream, device=dev)
-
-    # raw device pointers: the buffers are resident and synchronized above, so no per-step wait
-    # on torch's stream is needed (Engine._after_torch)
-    p_recs, p_in, p_aux, p_out, p_tags = (t.data_ptr() for t in (d_recs, d_in, d_aux, d_out, d_tags))
-
-    def step():
-        eng.seal_batch(p_recs, p_in, p_aux, p_out, p_tags, flags=flags, n=n)
-
-    def sync():
-        eng.sync()
-        torch.cuda.synchronize(dev)
-
-    # kernel time of the same steps from HIP events on the engine's stream
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    marks = {"n": 0}
-
-    def timed_step():
-        if marks["n"] == args.warmup:
-            eng.join()  # the interval holds exactly the timed steps' kernels
-            ev0.record(stream)
-        step()
-        marks["n"] += 1
-        if marks["n"] == args.warmup + args.steps:
-            eng.join()
-            ev1.record(stream)
-
-    wall = dist.timed_steps(timed_step, args.steps, args.warmup, sync, dev)
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
-
-    payload = batch["payload"]  # sum of AEAD lengths (content + type byte)
-    value = dist.whole_job_rate(payload, args.steps, wall, world)
-    alg_bytes = 2 * payload + 16 * n
-    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-
-    # ---- the decrypt half (Gcm::decrypt, gcm.rs:142-157, via record.rs:201-240) over the records
-    # just sealed: same records, same bytes per record (read L + 16-byte tag, write L) ----
-    opened = None
-    if not args.no_open:
-        orecs = open_descs(recs)
-        d_orecs = torch.from_numpy(orecs.view(np.uint8).copy()).to(dev)
-        d_pt = torch.zeros(batch["out_bytes"], dtype=torch.uint8, device=dev)
-        d_res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
-        torch.cuda.synchronize(dev)
-        q_recs, q_pt, q_res = d_orecs.data_ptr(), d_pt.data_ptr(), d_res.data_ptr()
-        o0, o1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for i in range(args.warmup + args.steps):
-            if i == args.warmup:
-                eng.join()
-                o0.record(stream)
-            eng.open_batch(q_recs, p_out, p_aux, p_tags, q_pt, q_res, flags=flags, n=n)
-        eng.join()
-        o1.record(stream)
-        sync()
-        open_ms = o0.elapsed_time(o1) / args.steps
-        res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
-        ok = bool((res["status"] == 0).all() and (res["content_len"] == recs["len"]).all()
-                  and (res["content_type"] == 23).all())
-        lens = recs["len"]
-        if ok and (lens == lens[0]).all() and (np.diff(recs["in_off"]) == recs["in_off"][1] - recs["in_off"][0]).all() \
-                and (np.diff(recs["out_off"]) == recs["out_off"][1] - recs["out_off"][0]).all():
-            # uniform records (C2-C4): every plaintext byte of every record against the sealed input
-            L, si, so = int(lens[0]), int(recs["in_off"][1] - recs["in_off"][0]), int(recs["out_off"][1] - recs["out_off"][0])
-            ok = bool(torch.equal(d_pt[: n * so].view(n, so)[:, :L], d_in[: n * si].view(n, si)[:, :L]))
-        open_alg = alg_bytes  # read L+1 ciphertext + 16 tag, write L+1 plaintext per record
-        open_ach = open_alg / (open_ms * 1e-3) / 1e9
-        opened = {"GiBps": round(payload / (open_ms * 1e-3) / 2**30, 3), "kernel_ms": round(open_ms, 4),
-                  "achieved_GBps": round(open_ach, 1), "frac": round(open_ach / HBM_PEAK_GBPS, 4),
-                  "plaintext_and_status_ok": ok,
-                  "what": "open_batch over the sealed records (device-resident, same batch), HIP events on the "
-                          "engine stream over the timed steps"}
-        del d_orecs, d_pt, d_res
+    # this rank's shard of the config's record stream (weak scaling: fixed records per GPU)
+    m = measure(args.config, eng, dev, rank, world, args.steps, args.warmup, not args.no_lazy_join,
+                records=args.records, key_slots=args.key_slots, keep=True)
+    batch, recs, n, payload = m["batch"], m["batch"]["recs"], m["n"], m["payload"]
+    d_in, d_out, d_tags, d_aux = m["d_in"], m["d_out"], m["d_tags"], m["d_aux"]
+    flags, stream, sync, kern_ms, achieved, alg_bytes = m["flags"], m["stream"], m["sync"], m["kern_ms"], m["achieved"], m["alg_bytes"]
 
     # measured on-device copy bandwidth: read + write of this batch's payload buffer
     d_cp = torch.empty_like(d_in)
@@ -399,12 +492,12 @@ def main():
         suite, _, clen = workload.CONFIGS[args.config]
         result = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": round(m["value"], 3),
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "ms_per_step": round(m["wall"] / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -419,9 +512,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes,
                          "copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(achieved / copy_gbps, 4)},
+            "open": m["open"],
         }
-        if opened is not None:
-            result["open"] = opened
         if world == 1 and not args.no_cpu_baseline:
             sample = min(n, 4096)
             h_in = d_in[: int(recs["in_off"][sample - 1]) + int(recs["len"][sample - 1]) + 16].cpu().numpy()
@@ -469,11 +561,13 @@ def main():
         w1.record(stream)
         sync()
         result["wire_GiBps"] = round(payload * args.steps / (w0.elapsed_time(w1) * 1e-3) / 2**30, 3)
+    del m, d_in, d_out, d_tags
+    torch.cuda.empty_cache()
     if world > 1 and not args.no_scatter:
-        # A batch arriving at one GPU: rank 0's shard is split by cumulative bytes
-        # over all ranks, scattered over RCCL, sealed by every rank's engine and gathered back
-        # (dist.seal_sharded); reported beside `value`, which is the pre-sharded rate. The result
-        # must equal rank 0's own single-GPU seal of the same records (d_out / d_tags above).
+        # A batch arriving at one GPU: the config's WHOLE batch (C4: 1 Mi records, 17 GB
+        # each way) on rank 0, split by cumulative bytes over all ranks, scattered over RCCL, sealed by
+        # every rank's engine and gathered back (dist.seal_sharded); reported beside `value`, which is
+        # the pre-sharded rate. The result must equal rank 0's own single-GPU seal of the whole batch.
         # A failed exchange is recorded in the line; a hung one fires the watchdog on every rank,
         # rank 0 first printing the line without it, and the process exits non-zero
         # (dist.WATCHDOG_EXIT): the measured line survives, and the status says something hung.
@@ -482,15 +576,37 @@ def main():
                 result["sharded_from_rank0"] = {"error": f"no result within {args.scatter_timeout:.0f} s"}
                 print(json.dumps(result), flush=True)
 
-        ok, sg = dist.run_or_exit(
-            lambda: sharded_exchange(args, eng, dev, d_in if rank == 0 else None, d_aux,
-                                     d_out if rank == 0 else None, d_tags if rank == 0 else None),
-            args.scatter_timeout, give_up)
+        def exchange():
+            whole = whole_batch(args, world)
+            eng.set_keys(whole["keys"])
+            g = torch.Generator(device=dev).manual_seed(workload.SEEDS["payload"])
+
+            def seal(rr, inp, o, t):
+                eng.seal_batch(rr, inp, d_aux, o, t, flags=atls.FLAG_DEVICE_PTRS)  # synchronous
+
+            return sharded_exchange(
+                whole, seal, lambda nb: torch.randint(0, 256, (nb,), dtype=torch.uint8, device=dev, generator=g),
+                lambda nb: torch.zeros(nb, dtype=torch.uint8, device=dev), lambda: torch.cuda.synchronize(dev), dev)
+
+        ok, sg = dist.run_or_exit(exchange, args.scatter_timeout, give_up)
         if not ok:
             print(f"sharded exchange failed: {sg}", file=sys.stderr, flush=True)
             sg = {"error": str(sg)[:200]}  # recorded in the line; the measured value stands
         if rank == 0 and result is not None:
             result["sharded_from_rank0"] = sg
+        torch.cuda.empty_cache()
+    if not args.no_configs:
+        # the other BASELINE configs, each rank its own shard, fewer steps
+        steps, warmup = min(args.steps, args.config_steps), min(args.warmup, 2)
+        cfgs = {}
+        for name in EXTRA_CONFIGS:
+            if name == args.config:
+                continue
+            mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join)
+            cfgs[name] = config_summary(name, mm, steps)
+            del mm
+        if rank == 0:
+            result["configs"] = cfgs
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()

@@ -32,6 +32,23 @@ def test_gpus_flag_launches_ranks(n):
     assert d["value"] > 0 and d["scaling"] == "weak"
 
 
+@pytest.mark.timeout(400)
+def test_whole_c4_batch_exchange_from_rank0_at_8_ranks():
+    """the sharded exchange (sharded_from_rank0) starts from the config's WHOLE batch on
+    rank 0 -- C4's 1,048,576 records -- not rank 0's own shard; split 8 ways by bytes (131,072 each for
+    C4's equal records), scattered, sealed by each rank (stub sealer on the CPU) and gathered back equal
+    to rank 0 sealing the whole batch alone. Contents cut to 16 B per record so it fits a CPU run."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--dry-run", "--config", "c4_aes256gcm_1Mi_x_16KiB",
+                        "--steps", "2", "--warmup", "1", "--dry-run-cap", "16"],
+                       capture_output=True, text=True, timeout=360, env=_env())
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    sg = json.loads(lines[0])["sharded_from_rank0"]
+    assert sg["records"] == 1048576 and sg["matches_single_gpu"] is True
+    assert sg["records_per_rank"] == [131072] * 8
+
+
 @pytest.mark.timeout(120)
 def test_world_size_mismatch_exits_nonzero():
     r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run"], capture_output=True, text=True,

@@ -230,3 +230,47 @@ def test_lazy_join_batches_equal_joined_batches(atls):
         assert h_pt[o:o + L].tobytes() == h_in[s:s + L].tobytes(), i
     eng.close()
     ref.close()
+
+
+def test_lazy_flag_with_engine_staged_descriptors_and_scratch_tags(atls):
+    """LAZY_JOIN with host descriptors (staged into the engine's one descriptor buffer) or
+    without a tags array (WIRE records, the engine's scratch tags) must not leave a side kernel reading
+    a buffer the next batch rewrites: such batches join like unflagged ones. Batches of different sizes
+    back to back, alternating the two records sets, each equal to a synchronous seal."""
+    import torch
+
+    from anothertls_amd import workload
+
+    dev = torch.device("cuda", 0)
+    full = workload.config_batch("c5_mixed_256Ki_x_64B-16KiB", n=2500)
+    eng = atls.Engine(0)
+    eng.set_keys(full["keys"])
+    g = torch.Generator(device=dev).manual_seed(11)
+    d_in = torch.randint(0, 256, (full["in_bytes"] + 16,), dtype=torch.uint8, device=dev, generator=g)
+    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+    wire = workload.wire_batch(full)
+    lazy = atls.FLAG_DEVICE_PTRS | atls.FLAG_NO_SYNC | atls.FLAG_LAZY_JOIN
+    cases = []
+    for n in (2500, 700, 2500, 1200, 300):
+        for kind in ("tls", "wire"):
+            recs = (full if kind == "tls" else wire)["recs"][:n].copy()
+            out_bytes = (full if kind == "tls" else wire)["out_bytes"] + 64
+            out = torch.zeros(out_bytes, dtype=torch.uint8, device=dev)
+            tags = torch.zeros(16 * n, dtype=torch.uint8, device=dev) if kind == "tls" else None
+            cases.append((recs, out, tags))
+    torch.cuda.synchronize()
+    for recs, out, tags in cases:  # host descriptors; WIRE batches without a tags array
+        eng.seal_batch(recs, d_in.data_ptr(), d_aux.data_ptr(), out.data_ptr(), None if tags is None else tags.data_ptr(),
+                       flags=lazy, n=len(recs))
+    eng.sync()
+    ref = atls.Engine(0)
+    ref.set_keys(full["keys"])
+    for recs, out, tags in cases:
+        r_out = torch.zeros_like(out)
+        r_tags = None if tags is None else torch.zeros_like(tags)
+        ref.seal_batch(recs, d_in, d_aux, r_out, r_tags, flags=atls.FLAG_DEVICE_PTRS)
+        assert torch.equal(out, r_out)
+        if tags is not None:
+            assert torch.equal(tags, r_tags)
+    ref.close()
+    eng.close()

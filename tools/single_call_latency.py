@@ -38,6 +38,25 @@ def main():
             out[f"{name}_{n}_open_us"] = _median_us(lambda: c.decrypt(key, iv, ct, b"\x17\x03\x03\x40\x11", tag), 200)
             out[f"{name}_{n}_oracle_seal_us"] = _median_us(
                 lambda: ora.cipher_encrypt(suite, key, iv, pt, b"\x17\x03\x03\x40\x11"), 5 if n > 2000 else 20)
+    # a fresh key on every call (the reference expands the key and computes H on every call, gcm.rs:49-56):
+    # 256 keys in turn, more than a context's 16 cached slots, so every call installs its key first
+    # (key-setup kernel, its key in the launch arguments) and then seals
+    aad = b"\x17\x03\x03\x06\x11"
+    for suite, klen, name in [(0x1301, 16, "aes128gcm"), (0x1302, 32, "aes256gcm"), (0x1303, 32, "chacha20poly1305")]:
+        c = atls.CipherSuite(suite).get_cipher()
+        keys = [os.urandom(klen) for _ in range(256)]
+        pt = os.urandom(1537)
+        it = {"i": 0}
+
+        def call():
+            it["i"] += 1
+            c.encrypt(keys[it["i"] % 256], iv, pt, aad)
+
+        out[f"{name}_1537_newkey_seal_us"] = _median_us(call, 400)
+        out[f"{name}_1537_oracle_newkey_seal_us"] = _median_us(
+            lambda: ora.cipher_encrypt(suite, keys[0], iv, pt, aad), 20)
+        ct, tag = c.encrypt(keys[5], iv, pt, aad)
+        assert ora.cipher_encrypt(suite, keys[5], iv, pt, aad)[1:] == (ct, tag)
     # 8 threads, each its own key, 16385-B AES-128-GCM seals
     calls, secs = 200, []
     pt = os.urandom(16385)
