@@ -184,6 +184,22 @@ struct ChArgs {
   uint32_t done_val;
 };
 
+// Phase clocks of the single call (timing build -DATLS_LAT_STAMPS, tools/single_call_stamps.py): lane 0
+// of a one-record 64-lane wave adds the shader clock at each point to g_lat_stamps[i] after waiting for
+// its outstanding memory operations (so a phase ends when its loads have landed); [8] / [9] hold the
+// 100 MHz real-time clock at entry / exit, [15] the call count.
+#ifdef ATLS_LAT_STAMPS
+__device__ unsigned long long g_lat_stamps[16];
+#define LAT_STAMP(i, lane0)                                                   \
+  do {                                                                        \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");               \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                         \
+    if (lane0) atomicAdd(&g_lat_stamps[i], (unsigned long long)t_);           \
+  } while (0)
+#else
+#define LAT_STAMP(i, lane0) do { } while (0)
+#endif
+
 // LATE: r^2 and r^3 for the lane combine are recomputed after the slot loop instead of living
 // through it (10 fewer VGPRs there, 2 more multiplies per record and lane). Same-box A/B over 3
 // rounds (profiles/r03/ab_chacha_late_pow.log): the open kernels and the planned seal kernel spill
@@ -195,7 +211,7 @@ struct ChArgs {
 // bytes [64 (base - 1), 64 (base + G - 1)), which starts 64 B before the slot grid, so unless the
 // output sits at (dst - 64) % 128 == 0 the window's last `mis` bytes share a 128-B line with the next
 // step's first bytes. Written at once, that line is written in two steps far apart and the L2 writes
-// it back twice (31 64-B writes per 24-segment record instead of 24.4, tools/_r3_traffic3.sh). With
+// it back twice (31 64-B writes per 24-segment record instead of 24.4, tools/recipes/sessions/_r3_traffic3.sh). With
 // CARRY those trailing 16-B pieces wait in LDS and are stored in the next step, beside the rest of
 // their line.
 // MAC_FIRST (opens; 1 = planned kernels, 2 = planned and direct): a data slot's ciphertext is folded
@@ -261,6 +277,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     aad_len = d.aad_len;
     aadp = iv + 12;
   }
+  if (G == 64) LAT_STAMP(1, gl == 0);  // descriptor, key words, nonce / AAD in registers
   const uint32_t na = tls ? 1u : (aad_len + 15u) / 16u;
   const uint32_t nct = (n + 15u) / 16u;         // ciphertext pieces (pad16, poly1305.rs:52-56)
   const uint32_t jmax = (n + 63u) / 64u;        // data blocks (f32 ceil is exact below 2^24)
@@ -325,6 +342,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 #pragma unroll
       for (int q = 0; q < 4; q++) pre[q] = ld16(src + 64u * (j - 1) + 16 * q);
     }
+    if (G == 64 && base == 0) LAT_STAMP(2, gl == 0);  // the step's data blocks loaded
     uint32_t ks[16];
     if (active && j <= jmax && (!MAC_FIRST || j == 0)) {
       if ((ATLS_CHACHA_DBG & 1) && j) {  // timing build: no keystream for data slots (wrong output)
@@ -334,6 +352,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         chacha_block(kw, j, nw, ks);
       }
     }
+    if (G == 64 && base == 0) LAT_STAMP(3, gl == 0);  // keystream blocks
     if (base == 0) {
       // Poly1305 one-time key from block 0 (poly1305.rs:19-22), broadcast within the group.
       uint32_t r0 = __shfl(ks[0], 0, G), r1 = __shfl(ks[1], 0, G), r2 = __shfl(ks[2], 0, G), r3 = __shfl(ks[3], 0, G);
@@ -356,6 +375,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         if (gl >= d) R = m;
       }
       r64 = shfl_p<G>(R, G - 1);
+      if (G == 64) LAT_STAMP(4, gl == 0);  // r powers (lane scan)
     }
     if (!active) continue;
     const uint4 cur0 = pre[0], cur1 = pre[1], cur2 = pre[2], cur3 = pre[3];
@@ -526,6 +546,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   }
 
   flush();
+  if (G == 64) LAT_STAMP(5, gl == 0);  // slots: XOR, stores issued, slot MACs
 
   // Lane partial: acc covers refs up to its last folded slot jf; contribution acc * r^(Q - ref).
   P130 contrib = p_zero();
@@ -559,6 +580,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   }
   uint32_t tag[4];
   p_finish(contrib, sk, tag);
+  if (G == 64) LAT_STAMP(6, gl == 0);  // lane combine, reduction, tag
 
   if (!OPEN) {
     if (gl == 0) {
@@ -796,9 +818,88 @@ __global__ __launch_bounds__(64) void chacha_kernel_lat(ChArgs A) {
   }
 }
 
+// The single call with its descriptor, IV || AAD, input and received tag in the launch's argument block
+// (kSingleInline bytes at most): the wave starts with everything but the key schedule (device memory)
+// at hand, where chacha_kernel_lat reads the descriptor from mapped host memory first and the key slot,
+// nonce / AAD and data after it -- dependent PCIe round trips before the first ChaCha round. Outputs,
+// tag, open result and the completion flag still go to the caller's mapped pinned block.
+struct ChSingle {
+  ChArgs A;
+  atls_rec d;          // in_off / aux_off relative to bytes
+  uint32_t tag_off;    // open: the received tag at bytes + tag_off
+  uint32_t pad[3];
+  uint8_t bytes[kSingleInline];
+};
+template <bool OPEN>
+__global__ __launch_bounds__(64) void chacha_single(ChSingle) {
+  // the argument block itself (the only explicit argument, at offset 0), read in place: naming the
+  // by-value parameter's members by address would copy all of it to scratch first
+  const ChSingle* S = (const ChSingle*)__builtin_amdgcn_kernarg_segment_ptr();
+  ChArgs A = S->A;
+  A.recs = &S->d;
+  A.in = S->bytes;
+  A.aux = S->bytes;
+  if (OPEN) A.tags_in = S->bytes + S->tag_off;
+  const WorkList W{nullptr, nullptr, kListChacha, 1u};
+#ifdef ATLS_LAT_STAMPS
+  if (threadIdx.x == 0) {
+    atomicAdd(&g_lat_stamps[8], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    atomicAdd(&g_lat_stamps[15], 1ull);
+  }
+  LAT_STAMP(0, threadIdx.x == 0);
+#endif
+  chacha_group<OPEN, 64, false>(A, W, 0u, 1u, (int)(threadIdx.x & 63));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#ifdef ATLS_LAT_STAMPS
+  LAT_STAMP(7, threadIdx.x == 0);  // outputs written to the caller's mapped memory
+  if (threadIdx.x == 0) atomicAdd(&g_lat_stamps[9], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
+  if ((threadIdx.x & 63) == 0) __hip_atomic_store(A.done, A.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace atls
 
-extern "C" unsigned atls_chacha_dbg(void) { return ATLS_CHACHA_DBG; }
+extern "C" unsigned atls_chacha_dbg(void) {
+#ifdef ATLS_LAT_STAMPS
+  return ATLS_CHACHA_DBG | 0x100u;  // a timing build (reported by atls_build_flags)
+#else
+  return ATLS_CHACHA_DBG;
+#endif
+}
+
+// Debug: copy out (and reset) the single call's phase clocks of a -DATLS_LAT_STAMPS build; -1 otherwise.
+extern "C" int atls_debug_lat_stamps(unsigned long long* out) {
+#ifdef ATLS_LAT_STAMPS
+  unsigned long long h[16], z[16] = {};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(atls::g_lat_stamps), sizeof(h)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(atls::g_lat_stamps), z, sizeof(z)) != hipSuccess) return -1;
+  for (int i = 0; i < 16; i++) out[i] = h[i];
+  return 0;
+#else
+  (void)out;
+  return -1;
+#endif
+}
+
+// One RAW record (the Cipher-trait single call) from the argument block: d's in_off / aux_off index
+// `bytes` (nbytes <= kSingleInline, IV || AAD || input || tag), outputs at out + d.out_off, tags_out,
+// res; done is set to done_val once they are visible.
+extern "C" int atls_launch_chacha_single(int open, const void* ks, uint32_t n_slots, const atls_rec* d,
+                                         const uint8_t* bytes, uint32_t nbytes, uint32_t tag_off, uint8_t* out,
+                                         uint8_t* tags_out, atls_open_result* res, uint32_t* err, uint32_t* done,
+                                         uint32_t done_val, hipStream_t s) {
+  if (nbytes > atls::kSingleInline || !done) return ATLS_INTERNAL_ERROR;
+  atls::ChSingle S;
+  S.A = atls::ChArgs{(const atls::KeySched*)ks, nullptr, 1u, nullptr, nullptr, out, tags_out, nullptr, res, nullptr,
+                     nullptr, err, n_slots, done, done_val};
+  S.d = *d;
+  S.tag_off = tag_off;
+  __builtin_memcpy(S.bytes, bytes, nbytes);
+  if (open) hipLaunchKernelGGL((atls::chacha_single<true>), dim3(1), dim3(64), 0, s, S);
+  else hipLaunchKernelGGL((atls::chacha_single<false>), dim3(1), dim3(64), 0, s, S);
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}
 
 // idx / plan: the batch plan's work lists (G = 16), or nullptr for a direct batch (per-step widths).
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,

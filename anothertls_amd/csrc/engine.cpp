@@ -40,6 +40,14 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
                                const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
 extern "C" size_t atls_group_hdr_offset(uint32_t n_slots);
+extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t n_slots, const atls_rec* d,
+                                      const uint8_t* bytes, uint32_t nbytes, uint32_t tag_off, uint8_t* out,
+                                      uint8_t* tags_out, atls_open_result* res, const uint32_t* t0, uint32_t* err,
+                                      uint32_t* done, uint32_t done_val, hipStream_t s);
+extern "C" int atls_launch_chacha_single(int open, const void* ks, uint32_t n_slots, const atls_rec* d,
+                                         const uint8_t* bytes, uint32_t nbytes, uint32_t tag_off, uint8_t* out,
+                                         uint8_t* tags_out, atls_open_result* res, uint32_t* err, uint32_t* done,
+                                         uint32_t done_val, hipStream_t s);
 extern "C" int atls_launch_group(const atls_rec* recs, uint32_t n, uint32_t n_slots, uint32_t* cnt, void* aux,
                                  uint32_t* gidx, int cus, hipStream_t s);
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,
@@ -734,6 +742,16 @@ size_t single_zero_copy_max() {
   return v;
 }
 
+// ATLS_SINGLE_INLINE=0 sends every single call through the pinned-block path (A/B of the argument-block
+// path, tests).
+bool single_inline() {
+  static const bool v = [] {
+    const char* e = std::getenv("ATLS_SINGLE_INLINE");
+    return !e || std::atoi(e) != 0;
+  }();
+  return v;
+}
+
 // 128-bit canary in the pinned tag slot of a seal: a kernel that refused the record leaves it in
 // place. Refusals cannot happen here (the descriptor is built and checked on the host exactly as
 // direct_reject checks it); the canary keeps a refusal from passing unnoticed all the same, at a
@@ -784,32 +802,59 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
   r.mode = ATLS_MODE_RAW;
   r.iv_len = (uint8_t)iv_len;
   r.aad_len = (uint16_t)aad_len;
-  std::memcpy(h + rec_at, &r, sizeof r);
+  // IV || AAD || input || tag that fit the launch's argument block go there with the descriptor
+  // (gcm_single / chacha_single): the kernel makes no dependent reads of mapped host memory before its
+  // first round. Longer records: the kernel reads descriptor and data from the pinned block (or a copy).
+  const size_t inl_in = (iv_len + aad_len + 15) & ~size_t(15), inl_tag = (inl_in + len + 15) & ~size_t(15);
+  const bool inl = single_inline() && inl_tag + (open ? 16 : 0) <= atls::kSingleInline;
   if (open) {
-    std::memcpy(h + tag_at, tag_in, 16);
     std::memset(h + res_at, 0xff, sizeof(atls_open_result));  // the kernel writes every field
   } else {
     std::memcpy(h + tag_at, kTagCanary, 16);
   }
-  if (iv_len) std::memcpy(h + aux_at, iv, iv_len);
-  if (aad_len) std::memcpy(h + aux_at + iv_len, aad, aad_len);
-  if (len) std::memcpy(h + in_at, in, len);
+  if (!inl) {
+    std::memcpy(h + rec_at, &r, sizeof r);
+    if (open) std::memcpy(h + tag_at, tag_in, 16);
+    if (iv_len) std::memcpy(h + aux_at, iv, iv_len);
+    if (aad_len) std::memcpy(h + aux_at + iv_len, aad, aad_len);
+    if (len) std::memcpy(h + in_at, in, len);
+  }
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
   hipStream_t s = e->stream;
   uint8_t* hd = c->pin_dev;
-  const uint8_t* src = hd;  // descriptor, aux, tag-in and input: read in place ...
-  if (len > single_zero_copy_max()) {  // ... or from one copy of the block
-    if (!e->in.reserve(out_at) || hipMemcpyAsync(e->in.p, h, out_at, hipMemcpyHostToDevice, s) != hipSuccess)
-      return ATLS_INTERNAL_ERROR;
-    src = (const uint8_t*)e->in.p;
-  }
   const uint32_t done_val = ++c->calls;
   // the flag word holds anything after a (re)allocation of the block: set it to a value other than
   // done_val, so only this launch's store ends the spin
   __atomic_store_n((uint32_t*)(h + done_at), done_val - 1u, __ATOMIC_RELEASE);
-  rc = launch_records(e, open, (const atls_rec*)(src + rec_at), 1, src, src, hd, hd + tag_at, src + tag_at,
-                      (atls_open_result*)(hd + res_at), s, (uint32_t*)(hd + done_at), done_val);
+  if (inl) {
+    uint8_t bytes[atls::kSingleInline];
+    if (iv_len) std::memcpy(bytes, iv, iv_len);
+    if (aad_len) std::memcpy(bytes + iv_len, aad, aad_len);
+    if (len) std::memcpy(bytes + inl_in, in, len);
+    if (open) std::memcpy(bytes + inl_tag, tag_in, 16);
+    atls_rec d = r;
+    d.in_off = inl_in;
+    d.aux_off = 0;
+    const uint32_t nbytes = (uint32_t)(inl_tag + (open ? 16 : 0));
+    rc = suite == ATLS_TLS_CHACHA20_POLY1305_SHA256
+             ? atls_launch_chacha_single(open, e->ks.p, e->n_slots, &d, bytes, nbytes, (uint32_t)inl_tag, hd,
+                                         hd + tag_at, (atls_open_result*)(hd + res_at), (uint32_t*)e->err.p,
+                                         (uint32_t*)(hd + done_at), done_val, s)
+             : atls_launch_gcm_single(open, (int)key_len / 4 + 6, e->ks.p, e->n_slots, &d, bytes, nbytes,
+                                      (uint32_t)inl_tag, hd, hd + tag_at, (atls_open_result*)(hd + res_at),
+                                      (const uint32_t*)e->t0.p, (uint32_t*)e->err.p, (uint32_t*)(hd + done_at),
+                                      done_val, s);
+  } else {
+    const uint8_t* src = hd;  // descriptor, aux, tag-in and input: read in place ...
+    if (len > single_zero_copy_max()) {  // ... or from one copy of the block
+      if (!e->in.reserve(out_at) || hipMemcpyAsync(e->in.p, h, out_at, hipMemcpyHostToDevice, s) != hipSuccess)
+        return ATLS_INTERNAL_ERROR;
+      src = (const uint8_t*)e->in.p;
+    }
+    rc = launch_records(e, open, (const atls_rec*)(src + rec_at), 1, src, src, hd, hd + tag_at, src + tag_at,
+                        (atls_open_result*)(hd + res_at), s, (uint32_t*)(hd + done_at), done_val);
+  }
   if (rc) return rc;
   // spin on the kernel's completion flag (visible once every output byte is); a stream that ends
   // without it (a fault) is reported by hipStreamQuery, checked every few thousand spins

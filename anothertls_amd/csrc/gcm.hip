@@ -1006,7 +1006,67 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   }
 }
 
+// The single call with its descriptor, IV || AAD, input and received tag in the launch's argument block
+// (kSingleInline bytes at most; chacha.hip chacha_single has the same layout): 4 waves build the T-tables,
+// wave 0 seals / opens the record and sets the completion flag. The record's key schedule (device memory)
+// is read as soon as the wave starts, not after a descriptor read from mapped host memory.
+struct GcmSingle {
+  GcmArgs A;
+  atls_rec d;          // in_off / aux_off relative to bytes
+  uint32_t tag_off;    // open: the received tag at bytes + tag_off
+  uint32_t pad[3];
+  uint8_t bytes[kSingleInline];
+};
+constexpr int kSingleWaves = 4;
+template <bool OPEN, int NR>
+__global__ __launch_bounds__(64 * kSingleWaves) void gcm_single(GcmSingle) {
+  // the argument block itself (the only explicit argument, at offset 0), read in place: naming the
+  // by-value parameter's members by address would copy all of it to scratch first
+  const GcmSingle* S = (const GcmSingle*)__builtin_amdgcn_kernarg_segment_ptr();
+  GcmArgs A = S->A;
+  A.recs = &S->d;
+  A.in = S->bytes;
+  A.aux = S->bytes;
+  if (OPEN) A.tags_in = S->bytes + S->tag_off;
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  smem[kTabBytes / 4 + threadIdx.x] = A.t0[threadIdx.x];  // 256 threads: T0 through the GHASH area
+  __syncthreads();
+  for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
+    const uint32_t v = smem[kTabBytes / 4 + (i >> 6)];
+    smem[i] = (i & 32) ? rotl32(v, 8) : v;
+  }
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x & 63;
+  gcm_one<NR, OPEN>(A, 0u, 4u * (uint32_t)(lane & 31), (uint32_t)kTabBytes, lane);
+  signal_done(A.done, A.done_val, lane);
+}
+
 }  // namespace atls
+
+extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t n_slots, const atls_rec* d,
+                                      const uint8_t* bytes, uint32_t nbytes, uint32_t tag_off, uint8_t* out,
+                                      uint8_t* tags_out, atls_open_result* res, const uint32_t* t0, uint32_t* err,
+                                      uint32_t* done, uint32_t done_val, hipStream_t s) {
+  if (nbytes > atls::kSingleInline || !done) return ATLS_INTERNAL_ERROR;
+  atls::GcmSingle S;
+  S.A = atls::GcmArgs{(const atls::KeySched*)ks, nullptr, 1u, nullptr, nullptr, out, tags_out, nullptr, res, t0,
+                      nullptr, nullptr, err, n_slots, nullptr, nullptr, done, done_val};
+  S.d = *d;
+  S.tag_off = tag_off;
+  __builtin_memcpy(S.bytes, bytes, nbytes);
+  const dim3 block(64 * atls::kSingleWaves);
+  const size_t lds = atls::lds_bytes(1);
+#define ATLS_SINGLE(NR)                                                                          \
+  if (open) hipLaunchKernelGGL((atls::gcm_single<true, NR>), dim3(1), block, lds, s, S);         \
+  else hipLaunchKernelGGL((atls::gcm_single<false, NR>), dim3(1), block, lds, s, S);
+  if (nr == 10) { ATLS_SINGLE(10) }
+  else if (nr == 12) { ATLS_SINGLE(12) }
+  else if (nr == 14) { ATLS_SINGLE(14) }
+  else return ATLS_INTERNAL_ERROR;
+#undef ATLS_SINGLE
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}
 
 // nr_mask: bit 0/1/2 = key slots with 10/12/14 rounds exist (one launch each). plan/idx: the
 // batch plan of atls_launch_plan, or idx = nullptr for a direct batch (one round count only; the

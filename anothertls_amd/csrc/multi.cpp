@@ -139,6 +139,17 @@ struct atls_multi {
 
 namespace {
 
+// Largest RCCL point-to-point message (ATLS_MULTI_CHUNK_MB, default 1024 MiB; 0 = none): larger ranges go
+// in several messages.
+size_t multi_xfer_chunk() {
+  static const size_t v = [] {
+    const char* e = std::getenv("ATLS_MULTI_CHUNK_MB");
+    const long mb = e ? std::atol(e) : 1024;
+    return mb > 0 ? (size_t)mb << 20 : ~size_t(0);
+  }();
+  return v;
+}
+
 // Wait for everything queued for this batch (engine streams, transfer streams), and clear the
 // part engines' sticky error words, so an early return never leaves work that reads or writes
 // the caller's buffers, and no refusal of this batch is reported by a later call.
@@ -205,6 +216,19 @@ int run_device(atls_multi* m, bool open, const atls_rec* recs, const uint32_t* f
       auto chk = [&](ncclResult_t r) {
         if (r != ncclSuccess && bad == ncclSuccess) bad = r;
       };
+      // Every send / recv pair in pieces of at most multi_xfer_chunk() bytes, matched in order on both
+      // sides: one C4 range is 2 GiB each way (131,072 x 16 KiB), and a single RCCL point-to-point
+      // message of 2^31 bytes or more came back wrong on the one-GPU self exchange
+      // (tests/test_gpu_c4_full.py, round 4).
+      const size_t piece = multi_xfer_chunk();
+      auto send = [&](const void* p, size_t bytes, int peer, ncclComm_t c, hipStream_t st) {
+        for (size_t o = 0; o < bytes; o += piece)
+          chk(R.send((const uint8_t*)p + o, std::min(piece, bytes - o), ncclUint8, peer, c, st));
+      };
+      auto recv = [&](void* p, size_t bytes, int peer, ncclComm_t c, hipStream_t st) {
+        for (size_t o = 0; o < bytes; o += piece)
+          chk(R.recv((uint8_t*)p + o, std::min(piece, bytes - o), ncclUint8, peer, c, st));
+      };
       for (size_t p = 1; p < P; p++) {
         Part& q = m->parts[p];
         const Range& r = rg[p];
@@ -215,28 +239,28 @@ int run_device(atls_multi* m, bool open, const atls_rec* recs, const uint32_t* f
         ncclComm_t rc = m->comms[0], qc = m->comms[m->rccl_self ? 0 : p];
         hipStream_t qs = side_stream(p);
         if (to_parts) {
-          chk(R.send(in + r.in_lo, r.in_hi - r.in_lo, ncclUint8, peer, rc, root.comm));
-          chk(R.recv(q.in.p, r.in_hi - r.in_lo, ncclUint8, 0, qc, qs));
-          chk(R.send(out + r.out_lo, r.out_hi - r.out_lo, ncclUint8, peer, rc, root.comm));  // bytes between records
-          chk(R.recv(q.out.p, r.out_hi - r.out_lo, ncclUint8, 0, qc, qs));
+          send(in + r.in_lo, r.in_hi - r.in_lo, peer, rc, root.comm);
+          recv(q.in.p, r.in_hi - r.in_lo, 0, qc, qs);
+          send(out + r.out_lo, r.out_hi - r.out_lo, peer, rc, root.comm);  // bytes between records
+          recv(q.out.p, r.out_hi - r.out_lo, 0, qc, qs);
           if (aux_end) {
-            chk(R.send(aux, aux_end, ncclUint8, peer, rc, root.comm));
-            chk(R.recv(q.aux.p, aux_end, ncclUint8, 0, qc, qs));
+            send(aux, aux_end, peer, rc, root.comm);
+            recv(q.aux.p, aux_end, 0, qc, qs);
           }
           if (open && tags_in) {
-            chk(R.send(tags_in + 16 * (size_t)r.a, 16 * (size_t)cnt, ncclUint8, peer, rc, root.comm));
-            chk(R.recv(q.tags.p, 16 * (size_t)cnt, ncclUint8, 0, qc, qs));
+            send(tags_in + 16 * (size_t)r.a, 16 * (size_t)cnt, peer, rc, root.comm);
+            recv(q.tags.p, 16 * (size_t)cnt, 0, qc, qs);
           }
         } else {
-          chk(R.send(q.out.p, r.out_hi - r.out_lo, ncclUint8, 0, qc, qs));
-          chk(R.recv(out + r.out_lo, r.out_hi - r.out_lo, ncclUint8, peer, rc, root.comm));
+          send(q.out.p, r.out_hi - r.out_lo, 0, qc, qs);
+          recv(out + r.out_lo, r.out_hi - r.out_lo, peer, rc, root.comm);
           if (!open && tags_out) {
-            chk(R.send(q.tags.p, 16 * (size_t)cnt, ncclUint8, 0, qc, qs));
-            chk(R.recv(tags_out + 16 * (size_t)r.a, 16 * (size_t)cnt, ncclUint8, peer, rc, root.comm));
+            send(q.tags.p, 16 * (size_t)cnt, 0, qc, qs);
+            recv(tags_out + 16 * (size_t)r.a, 16 * (size_t)cnt, peer, rc, root.comm);
           }
           if (open) {
-            chk(R.send(q.res.p, sizeof(atls_open_result) * (size_t)cnt, ncclUint8, 0, qc, qs));
-            chk(R.recv(res + r.a, sizeof(atls_open_result) * (size_t)cnt, ncclUint8, peer, rc, root.comm));
+            send(q.res.p, sizeof(atls_open_result) * (size_t)cnt, 0, qc, qs);
+            recv(res + r.a, sizeof(atls_open_result) * (size_t)cnt, peer, rc, root.comm);
           }
         }
       }

@@ -10,6 +10,9 @@ constexpr int kPlanClasses = 16;  // length classes min(len >> 10, 15), longest 
 constexpr uint32_t kPlanReject = 0xffu;
 constexpr uint32_t kPlanKeys = kPlanLists * kPlanClasses;  // work-list keys (list, length class)
 constexpr uint32_t kPlanMaxWG = 1024;                      // plan workgroups (2 per CU)
+// Single Cipher-trait calls (engine.cpp single): IV || AAD || input || received tag of up to this many
+// bytes travel in the launch's argument block (gcm_single / chacha_single), with the descriptor.
+constexpr uint32_t kSingleInline = 3584;
 
 struct PlanHdr {
   uint32_t off[kPlanLists + 1];                  // list l = idx[off[l] .. off[l+1])

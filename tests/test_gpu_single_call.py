@@ -117,3 +117,27 @@ def test_update_keys_keeps_other_slots():
     with pytest.raises(atls.TlsError):
         eng.update_keys(9, new)  # would leave a gap
     eng.close()
+
+
+@pytest.mark.parametrize("suite,klen", [(0x1301, 16), (0x1302, 24), (0x1302, 32), (0x1303, 32)])
+def test_argument_block_boundary_vs_oracle(suite, klen):
+    """Single calls whose IV || AAD || input (|| tag on open) fit the launch's argument block (3,584 B,
+    csrc/plan.h kSingleInline: gcm_single / chacha_single) and the first ones that do not (pinned-block
+    kernels), each side of the boundary, with 12- and 16-byte IVs (GCM) and 0..40-byte AADs."""
+    rng = random.Random(klen * 7 + suite)
+    key = bytes(rng.getrandbits(8) for _ in range(klen))
+    c = atls.CipherSuite(suite if suite != 0x1302 or klen == 32 else 0x1301).get_cipher()
+    for iv_len in ([12, 16] if suite != 0x1303 else [12]):
+        for aad_len in (0, 5, 40):
+            head = (iv_len + aad_len + 15) // 16 * 16
+            for n in (3584 - head - 32, 3584 - head - 17, 3584 - head - 16, 3584 - head - 1, 3584 - head, 3600):
+                iv = bytes(rng.getrandbits(8) for _ in range(iv_len))
+                aad = bytes(rng.getrandbits(8) for _ in range(aad_len))
+                pt = bytes(rng.getrandbits(8) for _ in range(n))
+                ct, tag = c.encrypt(key, iv, pt, aad)
+                rc, ect, etag = ora.cipher_encrypt(suite, key, iv, pt, aad)
+                assert rc == 0 and ct == ect and tag == etag, (iv_len, aad_len, n)
+                assert c.decrypt(key, iv, ct, aad, tag) == pt
+                with pytest.raises(atls.TlsError) as e:
+                    c.decrypt(key, iv, ct, aad, tag[:15] + bytes([tag[15] ^ 0x80]))
+                assert e.value.code == 20

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Timing-only A/B of anothertls_amd/variants/libatls_*.so (timing builds compute wrong results on purpose):
+# 3 interleaved rounds of the seal kernel time for each config in $CONFIGS.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"; mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+for round in 1 2 3; do
+  for lib in anothertls_amd/variants/libatls_*.so; do
+    n=$(basename $lib .so)
+    for c in ${CONFIGS:-c5_mixed_256Ki_x_64B-16KiB}; do
+      r=$(ATLS_LIB=$PWD/$lib timeout -k 10 120 python bench.py --config $c --no-cpu-baseline --no-open 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], 'seal', d['roofline']['kernel_ms'])") || exit 1
+      echo "round $round $n ${c%%_*}: $r"
+    done
+  done
+done

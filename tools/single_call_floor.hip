@@ -21,6 +21,20 @@ __global__ void empty_kernel(volatile uint32_t* flag, uint32_t v) {
   }
 }
 
+// (e) the same flag kernel with an argument block the size of the single-call kernels' (gcm_single /
+// chacha_single: descriptor + 3,584 inline bytes): the cost of carrying the record in the launch
+struct BigArgs {
+  uint32_t* flag;
+  uint32_t v;
+  uint8_t bytes[3712];
+};
+__global__ void empty_kernel_big(BigArgs a) {
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    *(volatile uint32_t*)a.flag = a.v + a.bytes[3711];
+  }
+}
+
 template <typename F>
 double median_us(F f, int reps) {
   f();
@@ -63,8 +77,20 @@ int main() {
     }
   }, 2000);
   (void)hipStreamSynchronize(s);
-  printf("{\"empty_launch_sync_us\": %.1f, \"empty_launch_flag_spin_us\": %.1f, \"empty_launch_writevalue_spin_us\": %.1f",
-         sync_us, spin_us, wv_us);
+  BigArgs big;
+  memset(&big, 0, sizeof big);
+  big.flag = dflag;
+  const double big_us = median_us([&] {
+    ++it;
+    big.v = it;
+    hipLaunchKernelGGL(empty_kernel_big, dim3(1), dim3(64), 0, s, big);
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != it) {
+    }
+  }, 2000);
+  (void)hipStreamSynchronize(s);
+  printf("{\"empty_launch_sync_us\": %.1f, \"empty_launch_flag_spin_us\": %.1f, \"empty_launch_writevalue_spin_us\": %.1f, "
+         "\"empty_launch_3712B_args_flag_spin_us\": %.1f",
+         sync_us, spin_us, wv_us, big_us);
   std::vector<uint8_t> key(32, 7), iv(12, 1), aad = {0x17, 3, 3, 0x06, 0x11}, tag(16);
   for (uint16_t suite : {(uint16_t)ATLS_TLS_CHACHA20_POLY1305_SHA256, (uint16_t)ATLS_TLS_AES_128_GCM_SHA256}) {
     const size_t kl = suite == ATLS_TLS_AES_128_GCM_SHA256 ? 16 : 32;
