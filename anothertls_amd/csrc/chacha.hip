@@ -240,7 +240,7 @@ typedef uint32_t v4u32_ch __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4u32_ch lds_uint4;
 // PRE: 0 = a slot's data is loaded where it is used (after its keystream); 1 = at the top of its step,
 // before the keystream; 2 = one step ahead, before the previous step's stores (chacha_kernel_w2).
-template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G == 64 ? 1 : 0>
+template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G == 64 ? 1 : 0, bool STAGE = false>
 __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl,
                               lds_uint4* lds = nullptr) {
   // TLS and WIRE: nonce from (static IV, seq), 5-byte AAD; WIRE also frames the record
@@ -308,6 +308,36 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     }
   };
 
+  // STAGE (round 4 A/B of VERDICT r3 #6; seals in waves whose records all take the same steps): a step's
+  // whole output blocks wait in the lane's LDS slots and go out at the top of the next step, transposed so
+  // that lanes 8k..8k+7 of one store instruction write one record's 128 contiguous bytes (the two lanes'
+  // blocks), not two 16-B pieces of each of 32 records. Collective: every lane of the wave runs it.
+  uint4 sb[4] = {};
+  uint8_t* sdst = nullptr;
+  bool sv = false;
+  auto stage_flush = [&]() {
+    if constexpr (STAGE) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) lds[q] = v4u32_ch{sb[q].x, sb[q].y, sb[q].z, sb[q].w};
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      const int lane = (int)(threadIdx.x & 63);
+      lds_uint4* wbase = lds - 4 * lane;
+      const uint64_t pd = reinterpret_cast<uint64_t>(sdst);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int sl = 16 * q + lane / 4;  // source lane; piece lane % 4 of its block
+        const v4u32_ch v = wbase[64 * q + lane];
+        const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)pd, sl, 64), hi = (uint32_t)__shfl((int)(uint32_t)(pd >> 32), sl, 64);
+        const int f = __shfl((int)sv, sl, 64);
+        if (f) st16(reinterpret_cast<uint8_t*>(((uint64_t)hi << 32) | lo) + 16 * (lane & 3), make_uint4(v.x, v.y, v.z, v.w));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+      sv = false;
+    }
+  };
+
   // PRE >= 2: every lane loads 64 B per step whatever its slot (a whole block of the slot PRE - 1 steps
   // ahead, or the always-readable key schedule): an unconditional load keeps the compiler's s_waitcnt
   // for the current block from waiting on the prefetches too. ring[0] is the current step's block.
@@ -327,6 +357,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     }
   }
   for (uint32_t base = 0; base <= jL; base += G) {
+    stage_flush();  // STAGE: the previous step's blocks (every lane, before any lane-dependent branch)
     const uint32_t j = base + (uint32_t)gl;
     const bool active = j <= jL;
     // Latency path (G = 64, one record per wave, the single call): the block's data is loaded before
@@ -489,7 +520,11 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 #pragma unroll
           for (int q = 0; q < 4; q++) {
             const uint4 v = make_uint4(P[4 * q], P[4 * q + 1], P[4 * q + 2], P[4 * q + 3]);
-            if (CARRY && mis && off + 16u * q >= thr) {
+            if (STAGE) {
+              sb[q] = v;
+              sdst = dst + off;
+              sv = true;
+            } else if (CARRY && mis && off + 16u * q >= thr) {
               lds[q] = v4u32_ch{v.x, v.y, v.z, v.w};
               cmask |= 1u << q;
               coff = off;
@@ -546,6 +581,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   }
 
   flush();
+  stage_flush();
   if (G == 64) LAT_STAMP(5, gl == 0);  // slots: XOR, stores issued, slot MACs
 
   // Lane partial: acc covers refs up to its last folded slot jf; contribution acc * r^(Q - ref).
@@ -629,7 +665,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 
 // One group of G lanes seals / opens the record at work-list position q (direct batches: the
 // kernel validates the descriptor itself).
-template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G == 64 ? 1 : 0>
+template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G == 64 ? 1 : 0, bool STAGE = false>
 __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W, uint32_t q, uint32_t cnt, int gl,
                                              lds_uint4* lds = nullptr) {
   if (q >= cnt) return;
@@ -645,7 +681,7 @@ __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W,
       }
     }
   } else {
-    chacha_record<OPEN, G, LATE, CARRY, PRE>(A, d, A.ks + d.key_slot, r, gl, lds);
+    chacha_record<OPEN, G, LATE, CARRY, PRE, STAGE>(A, d, A.ks + d.key_slot, r, gl, lds);
   }
 }
 
@@ -739,6 +775,9 @@ __device__ __forceinline__ void chacha_batch(const ChArgs& A, int lane) {
 #ifndef ATLS_CHACHA_W2
 #define ATLS_CHACHA_W2 1
 #endif
+#ifndef ATLS_CHACHA_STAGE
+#define ATLS_CHACHA_STAGE 0  // 1: whole-line transposed stores through LDS in the 2-wave seal kernel (A/B, chacha_record STAGE)
+#endif
 #ifndef ATLS_CHACHA_W2_PRE
 #define ATLS_CHACHA_W2_PRE 2  // 1: load a slot's data at the top of its step; 2: one step ahead (C3 open 0.0962 ->
                               // 0.0926 ms, seal 0.0834 -> 0.0806 ms: profiles/r03/ab_c3_pf.log)
@@ -768,6 +807,27 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
 #pragma unroll
     for (int off = (int)P / 2; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
     mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
+    if (ATLS_CHACHA_STAGE && !OPEN && PRE >= 2 && ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY &&
+        q0 + P <= cnt) {
+      // STAGE needs every lane in the same steps: a full wave step of TLS / RAW records of one length,
+      // none refused (else the unstaged path below)
+      uint32_t mn = 0xffffffffu, ok = 1u;
+      if ((uint32_t)lane < P) {
+        const atls_rec d = A.recs[q0 + (uint32_t)lane];
+        mn = d.len;
+        ok = (d.mode != ATLS_MODE_WIRE && d.mode == A.recs[q0].mode && !direct_reject(d, A.ks, A.n_slots, OPEN)) ? 1u : 0u;
+      }
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, off, 64));
+        ok &= (uint32_t)__shfl_xor((int)ok, off, 64);
+      }
+      if (__builtin_amdgcn_readfirstlane((int)(ok && mn == mx))) {
+        constexpr int G = ATLS_CHACHA_TINY_G;
+        chacha_group<OPEN, G, LATE, false, PRE, true>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);
+        continue;
+      }
+    }
     if (ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY) {
       constexpr int G = ATLS_CHACHA_TINY ? ATLS_CHACHA_TINY_G : 4;
       chacha_group<OPEN, G, LATE, (OPEN ? (PRE >= 2 ? ATLS_CHACHA_W2_CARRY_OPEN : ATLS_CHACHA_CARRY_OPEN) : ATLS_CHACHA_CARRY_SEAL), PRE>(A, W, q0 + (uint32_t)lane / (uint32_t)G, cnt, lane & (G - 1), lds);

@@ -50,6 +50,10 @@ namespace atls {
 #define ATLS_CTR_CACHE 1
 #endif
 
+#ifndef ATLS_GCM_FAST_FIRST
+#define ATLS_GCM_FAST_FIRST 0  // 1: a TLS record's first step (E_K(J0), AAD, 62 data blocks) without the general step's
+                               // classification, when it holds 62 whole blocks (round 4 A/B on C5)
+#endif
 #ifndef ATLS_PREFETCH
 #define ATLS_PREFETCH 1  // fast steps load the next step's data block before their own AES rounds
 #endif
@@ -427,6 +431,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   uint4 Pn = make_uint4(0u, 0u, 0u, 0u);
   bool pref = false;
   const uint32_t lim = min(in_bytes, n_aead);
+  const bool first_fast = ATLS_GCM_FAST_FIRST && use_cache && tls && !(OPEN && wire) && fast_end >= 64u;
   TT_STAMP(t_setup);
   for (uint32_t base = 0; base < S; base += 64) {
     TT_STAMP(t_step);
@@ -459,6 +464,30 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       t_fast += __builtin_amdgcn_s_memtime() - t_step;
       n_fast++;
 #endif
+      continue;
+    }
+    if (ATLS_GCM_FAST_FIRST && base == 0u && first_fast) {
+      // The first step without classification (round 4 A/B): lane 0 E_K(J0) (counter 1),
+      // lane 1 the TLS AAD block, lanes 2..63 data blocks 0..61 (counters 2..63) -- whole blocks when
+      // the record has at least 62 of them. Same counter cache as the fast steps (ctr >> 8 = 0).
+      const uint32_t off = lane >= 2 ? ((uint32_t)lane - 2u) * 16u : 0u;
+      const uint4 Pu = ld16(src + off);
+      if (ATLS_PREFETCH) {  // the next step's block, as a fast step loads it
+        const uint32_t offn = ((uint32_t)lane + 62u) * 16u;
+        pref = 128u <= fast_end;
+        Pn = ld16(src + (offn + 16u <= lim ? offn : off));
+      }
+      uint32_t st[4];
+      const uint32_t lo = lane == 0 ? 1u : (uint32_t)lane;  // the counter's low byte (J0 for lane 0)
+      aes_cached(st, ((lo << 8) | lb) ^ (k15 << 8), 0u);
+      const v4u32 C = {Pu.x ^ st[0], Pu.y ^ st[1], Pu.z ^ st[2], Pu.w ^ st[3]};
+      if (lane >= 2) st16(dst + off, make_uint4(C.x, C.y, C.z, C.w));
+      if (OPEN && lane >= 2) lastnz = block_last_nz(C.x, C.y, C.z, C.w, off, lastnz);
+      if (lane == 0) { e0 = st[0]; e1 = st[1]; e2 = st[2]; e3 = st[3]; }
+      if (lane == 1) { y[0] = hdr0; y[1] = hdr1; }  // Y = 0 before the first step: Y = B
+      if (lane >= 2) {
+        y[0] = OPEN ? Pu.x : C.x; y[1] = OPEN ? Pu.y : C.y; y[2] = OPEN ? Pu.z : C.z; y[3] = OPEN ? Pu.w : C.w;
+      }
       continue;
     }
     pref = false;

@@ -131,6 +131,26 @@ def extents(recs, open_=False):
     return L, np.where(mode == 1, L, np.where(mode == 2, L + 22, L + 1))
 
 
+# Largest point-to-point message: RCCL 2.26 (the librccl PyTorch ships here) returned wrong bytes past the
+# first GiB of a single 2 GiB send / recv (tools/multi_diag.py, profiles/r04/multi_diag.log: every record
+# in the second half of each 2 GiB C4 range), so ranges travel in pieces of at most 1 GiB, matched in
+# order on both sides. csrc/multi.cpp cuts its RCCL transfers the same way.
+P2P_PIECE = 1 << 30
+
+
+def _pieces(t):
+    n = t.numel()
+    return [t[o:o + P2P_PIECE] for o in range(0, n, P2P_PIECE)] or [t]
+
+
+def isend_pieces(t, dst):
+    return [tdist.isend(p, dst=dst) for p in _pieces(t)]
+
+
+def irecv_pieces(t, src):
+    return [tdist.irecv(p, src=src) for p in _pieces(t)]
+
+
 def seal_sharded(seal, recs, inp=None, out=None, tags=None, device=None):
     """Seal one batch that arrives at rank 0 with every rank's GPU: the records are cut into
     contiguous ranges balanced by cumulative bytes (atls_partition, the split the C ABI's
@@ -162,7 +182,7 @@ def seal_sharded(seal, recs, inp=None, out=None, tags=None, device=None):
         for r in range(1, world):
             ra, rb, ilo, ihi, olo, ohi = span(r)
             if ra < rb:
-                reqs += [tdist.isend(inp[ilo:ihi], dst=r), tdist.isend(out[olo:ohi], dst=r)]
+                reqs += isend_pieces(inp[ilo:ihi], r) + isend_pieces(out[olo:ohi], r)
         if a < b:
             seal(recs[a:b], inp, out, tags[16 * a:16 * b])
         for q in reqs:
@@ -171,7 +191,7 @@ def seal_sharded(seal, recs, inp=None, out=None, tags=None, device=None):
         for r in range(1, world):
             ra, rb, ilo, ihi, olo, ohi = span(r)
             if ra < rb:
-                reqs += [tdist.irecv(out[olo:ohi], src=r), tdist.irecv(tags[16 * ra:16 * rb], src=r)]
+                reqs += irecv_pieces(out[olo:ohi], r) + irecv_pieces(tags[16 * ra:16 * rb], r)
         for q in reqs:
             q.wait()
     elif a < b:
@@ -180,14 +200,14 @@ def seal_sharded(seal, recs, inp=None, out=None, tags=None, device=None):
         loc_in = torch.empty(in_hi - in_lo, dtype=torch.uint8, device=device)
         loc_out = torch.empty(out_hi - out_lo, dtype=torch.uint8, device=device)
         loc_tags = torch.empty(16 * (b - a), dtype=torch.uint8, device=device)
-        tdist.recv(loc_in, src=0)
-        tdist.recv(loc_out, src=0)
+        for q in irecv_pieces(loc_in, 0) + irecv_pieces(loc_out, 0):
+            q.wait()
         local = recs[a:b].copy()
         local["in_off"] -= np.uint64(in_lo)
         local["out_off"] -= np.uint64(out_lo)
         seal(local, loc_in, loc_out, loc_tags)
-        tdist.send(loc_out, dst=0)
-        tdist.send(loc_tags, dst=0)
+        for q in isend_pieces(loc_out, 0) + isend_pieces(loc_tags, 0):
+            q.wait()
     return a, b
 
 

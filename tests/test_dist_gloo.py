@@ -49,6 +49,7 @@ def _worker(rank, world, port, q):
     from anothertls_amd import dist, workload
 
     assert dist.init("gloo")
+    dist.P2P_PIECE = 777  # every range goes in several point-to-point pieces (the 1 GiB cap, scaled down)
     batch = workload.config_batch(CONFIG, n=N_RECORDS)
     inp = out = tags = None
     if rank == 0:
