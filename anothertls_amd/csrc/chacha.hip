@@ -399,6 +399,9 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       if (!LATE) rcu = p_mul(rsq, r);
 #pragma unroll
       for (int d = 1; d < G; d <<= 1) {  // Hillis-Steele prefix product
+        // one record per wave (the single call): lanes past jL hold no slot, so a record of one step
+        // (jL < 32: up to ~1.9 KiB) stops after the levels lanes 0..jL need (5 for an MTU-sized record)
+        if (G == 64 && (uint32_t)d > jL) continue;
         P130 t;
 #pragma unroll
         for (int i = 0; i < 5; i++) t.l[i] = __shfl_up(R.l[i], (unsigned)d, G);

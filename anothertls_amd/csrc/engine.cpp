@@ -29,7 +29,7 @@ extern "C" int atls_launch_build_t0(uint32_t* t0, hipStream_t s);
 extern "C" int atls_launch_aes_blocks(int decrypt, const void* ks, const uint8_t* in, uint8_t* out, uint64_t nblocks,
                                       uint32_t* err, int grid, hipStream_t s);
 extern "C" int atls_launch_key_setup(const atls_key* keys, const atls_key* host_keys, uint32_t n, void* ks,
-                                     hipStream_t s);
+                                     const uint32_t* t0, hipStream_t s);
 extern "C" int atls_key_setup_inline_max(void);
 extern "C" int atls_launch_plan(int open, const void* ks, const atls_rec* recs, uint32_t n, uint32_t n_slots,
                                 atls_open_result* res, uint32_t* err, void* P, uint8_t* keys, uint32_t* idx,
@@ -568,7 +568,7 @@ int install_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t 
       return ATLS_INTERNAL_ERROR;
   }
   if (atls_launch_key_setup(inl ? nullptr : (const atls_key*)e->keys_stage.p, keys, n, (atls::KeySched*)e->ks.p + first,
-                            e->stream))
+                            (const uint32_t*)e->t0.p, e->stream))
     return ATLS_INTERNAL_ERROR;
   if (!inl && hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
   if (replace) e->keys.clear();

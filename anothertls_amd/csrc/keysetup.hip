@@ -123,27 +123,96 @@ __device__ __forceinline__ void expand_and_h(const uint32_t (&kw)[8], const uint
                rk[4 * NR + c];
 }
 
+#ifndef ATLS_KS_ONE
+#define ATLS_KS_ONE 1  // a single key takes key_setup_kernel<true> (squared factors, all tables at once)
+#endif
+
 // Up to kInlineKeys keys travel in the kernel arguments (a connection's new key: no staging copy).
 constexpr int kInlineKeys = 4;
 constexpr int kSetupWaves = 4;                 // keys per workgroup
 constexpr uint32_t kSetupTab = 8192;           // one 4-bit table per wave
 constexpr uint32_t kSetupT0 = kSetupWaves * kSetupTab;
+constexpr int kOneTabs = 6;                    // ONE: the tables of H^(2^b), b = 0..5
+constexpr uint32_t kOneT0 = kOneTabs * kSetupTab;
 struct KeySetupArgs {
   const atls_key* keys;  // device array, or nullptr: the keys are in `inl`
   uint32_t n;
   KeySched* ks;
+  const uint32_t* t0;    // the engine's T0 (gcm.hip's table, built at engine creation)
   uint32_t inl[kInlineKeys][16];
 };
 static_assert(sizeof(atls_key) == 64, "atls_key is 16 words");
 
+// v <- v^2 in GF(2^128), be words. Squaring is linear: the coefficient of x^i moves to x^(2i), i.e. bit
+// b of each 64-bit half to bit 2b+1 of 128 bits; the high half's image stands for O(x) * x^128 =
+// O(x) * (1 + x + x^2 + x^7), folded back with the reducing shifts of gf_mulxk64.
+__device__ __forceinline__ uint64_t spread32(uint32_t x) {  // bit b -> bit 2b
+  uint64_t v = x;
+  v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+  v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+  v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  v = (v | (v << 2)) & 0x3333333333333333ull;
+  v = (v | (v << 1)) & 0x5555555555555555ull;
+  return v;
+}
+__device__ __forceinline__ void gf_square(uint32_t (&v)[4]) {
+  // low half x^0..x^63 (words 0, 1) -> x^0..x^126; high half x^64..x^127 (words 2, 3) -> O(x) * x^128
+  const uint64_t a_hi = spread32(v[0]) << 1, a_lo = spread32(v[1]) << 1;
+  const uint64_t o_hi = spread32(v[2]) << 1, o_lo = spread32(v[3]) << 1;
+  uint32_t o[4] = {(uint32_t)(o_hi >> 32), (uint32_t)o_hi, (uint32_t)(o_lo >> 32), (uint32_t)o_lo};
+  uint32_t o1[4] = {o[0], o[1], o[2], o[3]}, o2[4] = {o[0], o[1], o[2], o[3]}, o7[4] = {o[0], o[1], o[2], o[3]};
+  gf_mulxk64(o1, 1);
+  gf_mulxk64(o2, 2);
+  gf_mulxk64(o7, 7);
+  v[0] = (uint32_t)(a_hi >> 32) ^ o[0] ^ o1[0] ^ o2[0] ^ o7[0];
+  v[1] = (uint32_t)a_hi ^ o[1] ^ o1[1] ^ o2[1] ^ o7[1];
+  v[2] = (uint32_t)(a_lo >> 32) ^ o[2] ^ o1[2] ^ o2[2] ^ o7[2];
+  v[3] = (uint32_t)a_lo ^ o[3] ^ o1[3] ^ o2[3] ^ o7[3];
+}
+
+// Phase clocks of a key install (timing build -DATLS_KS_STAMPS, tools/key_setup_stamps.py): lane 0 of wave
+// 0 of key 0 adds the shader clock at each phase end (after its memory operations) to g_ks_stamps[i];
+// [14] / [15] the 100 MHz real-time clock at entry / exit, [13] the launch count.
+#ifdef ATLS_KS_STAMPS
+__device__ unsigned long long g_ks_stamps[16];
+#define KS_STAMP(i)                                                                          \
+  do {                                                                                       \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                              \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                                        \
+    if (i_key == 0 && threadIdx.x == 0) atomicAdd(&g_ks_stamps[i], (unsigned long long)t_);  \
+  } while (0)
+#else
+#define KS_STAMP(i) do { } while (0)
+#endif
+
+// ONE (a single key: the latency of a connection's new key, the single call's cache miss; round 4,
+// tools/key_setup_stamps.py, profiles/r04/key_setup_stamps.json): the per-wave scan spends ~1.1 us per level
+// on a table build and a product (six levels). Here the factors H^(2^b) come from squarings (linear: a bit
+// spread and one fold, no table), the four waves build all six factor tables at once (48 KiB), and lane l
+// forms H^(l+1) as the product of the factors of l + 1's set bits -- six table products and no build
+// between them. H^64 is the sixth square. The record-table seeds (x^(4p) * H^8 / H^16 / H^32 / H^64) need
+// only the factors, so waves 1-3 write them while wave 0 forms the powers. (Base-4 digits -- two products
+// per lane from tables of H^(j 4^k) -- measured slower: the H^3 they need took a comb multiply that cost
+// more at one wave than the four products it saved.)
+template <bool ONE>
 __global__ __launch_bounds__(64 * kSetupWaves) void key_setup_kernel(KeySetupArgs A) {
   extern __shared__ __attribute__((aligned(256))) uint32_t smem[];
-  uint32_t* t0 = smem + kSetupT0 / 4;
-  t0[threadIdx.x] = t0_entry((int)threadIdx.x);
-  __syncthreads();
   const int wave = (int)uni(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
-  const uint32_t i = blockIdx.x * kSetupWaves + (uint32_t)wave;
+  const uint32_t i = ONE ? 0u : blockIdx.x * kSetupWaves + (uint32_t)wave;
+#ifdef ATLS_KS_STAMPS
+  const uint32_t i_key = blockIdx.x;
+  if (i_key == 0 && threadIdx.x == 0) {
+    atomicAdd(&g_ks_stamps[14], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    atomicAdd(&g_ks_stamps[13], 1ull);
+  }
+  KS_STAMP(0);
+#endif
+  uint32_t* t0 = smem + (ONE ? kOneT0 : kSetupT0) / 4;
+  t0[threadIdx.x] = A.t0[threadIdx.x];  // one load per thread of a table the engine already holds
+  __syncthreads();
+  KS_STAMP(1);
   if (i >= A.n) return;
+  const bool writer = !ONE || wave == 0;  // the wave that stores the key's per-slot fields
   // the key's 16 words (atls_key: suite | key_len | iv_len, key[32], static_iv[12], reserved)
   uint32_t k[16];
   if (A.keys) {
@@ -160,7 +229,7 @@ __global__ __launch_bounds__(64 * kSetupWaves) void key_setup_kernel(KeySetupArg
   for (int q = 0; q < 8; q++) kw[q] = k[1 + q];
   // ChaCha20 key words and the static IV for every slot (the GCM kernels read siv too): word q of each
   // from lane q (selects, no indexed register access)
-  {
+  if (writer) {
     uint32_t kq = 0, sq = 0;
 #pragma unroll
     for (int q = 0; q < 8; q++) kq = lane == q ? kw[q] : kq;
@@ -171,7 +240,7 @@ __global__ __launch_bounds__(64 * kSetupWaves) void key_setup_kernel(KeySetupArg
   }
   const bool aes = (suite == kSuiteAes128 || suite == kSuiteAes256) && (key_len == 16 || key_len == 24 || key_len == 32);
   if (!aes) {
-    if (lane == 0) {
+    if (writer && lane == 0) {
       o->suite = suite;
       o->nr = 0;
       o->key_len = key_len;
@@ -179,12 +248,14 @@ __global__ __launch_bounds__(64 * kSetupWaves) void key_setup_kernel(KeySetupArg
     }
     return;
   }
+  KS_STAMP(2);
   uint32_t rk[60], h[4];
   if (key_len == 16) expand_and_h<4>(kw, t0, rk, h);
   else if (key_len == 24) expand_and_h<6>(kw, t0, rk, h);
   else expand_and_h<8>(kw, t0, rk, h);
+  KS_STAMP(3);
   const uint32_t nr = key_len / 4 + 6;
-  {  // round key w from lane w (one coalesced store each for rk and rkr)
+  if (writer) {  // round key w from lane w (one coalesced store each for rk and rkr)
     uint32_t mine = 0;
 #pragma unroll
     for (int w = 0; w < 60; w++) mine = lane == w ? rk[w] : mine;
@@ -196,47 +267,110 @@ __global__ __launch_bounds__(64 * kSetupWaves) void key_setup_kernel(KeySetupArg
   uint32_t hb[4];
 #pragma unroll
   for (int w = 0; w < 4; w++) hb[w] = bswap32(h[w]);
-  if (lane < 4) o->h_be[lane] = lane == 0 ? hb[0] : lane == 1 ? hb[1] : lane == 2 ? hb[2] : hb[3];
-  // H^(lane+1): doubling scan, each level's products by a table of the level's one factor H^(2^k)
-  const uint32_t wb = (uint32_t)wave * kSetupTab;
+  if (writer && lane < 4) o->h_be[lane] = lane == 0 ? hb[0] : lane == 1 ? hb[1] : lane == 2 ? hb[2] : hb[3];
+  KS_STAMP(4);
   uint32_t P[4] = {hb[0], hb[1], hb[2], hb[3]};
+  if constexpr (ONE) {
+    // F[b] = H^(2^b), b = 0..6, by squarings, wave-uniform (every wave squares the same values; in SGPRs)
+    uint32_t F[7][4];
+#pragma unroll
+    for (int w = 0; w < 4; w++) F[0][w] = uni(hb[w]);
+#pragma unroll
+    for (int b = 1; b < 7; b++) {
+#pragma unroll
+      for (int w = 0; w < 4; w++) F[b][w] = F[b - 1][w];
+      gf_square(F[b]);
+    }
+    // the six factor tables: 6 x 32 positions x 2 halves = 384 units over the 256 threads
+#pragma unroll
+    for (int u = (int)threadIdx.x; u < 2 * 32 * kOneTabs; u += 64 * kSetupWaves) {
+      const int b = u >> 6, p = (u >> 1) & 31;
+      uint32_t seed[4];
+#pragma unroll
+      for (int w = 0; w < 4; w++) seed[w] = b == 0 ? F[0][w] : b == 1 ? F[1][w] : b == 2 ? F[2][w] : b == 3 ? F[3][w]
+                                               : b == 4 ? F[4][w] : F[5][w];
+      gf_mulxk(seed, 4u * (uint32_t)p);
+      ghash_table_entries<8>((uint32_t)b * kSetupTab, seed, p, (u & 1) * 8);
+    }
+    __syncthreads();
+    KS_STAMP(5);
+    if (wave == 0) {
+      // H^(l+1) = product of F[b] over the set bits b of l + 1 (lane 63: H^64 = F[6])
+      const uint32_t e = (uint32_t)lane + 1u;
+      uint32_t acc[4] = {0x80000000u, 0u, 0u, 0u};  // 1 = x^0
+#pragma unroll
+      for (int b = 0; b < kOneTabs; b++) {
+        uint32_t x[4] = {acc[0], acc[1], acc[2], acc[3]};
+        table_mul(x, (uint32_t)b * kSetupTab);  // every lane runs the product; the bit decides
+        if ((e >> b) & 1u) {
+#pragma unroll
+          for (int w = 0; w < 4; w++) acc[w] = x[w];
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < 4; w++) P[w] = lane == 63 ? F[6][w] : acc[w];
+      *reinterpret_cast<uint4*>(o->hpow_be[lane]) = make_uint4(P[0], P[1], P[2], P[3]);
+    } else {
+      // seeds x^(4p) * H^64 (p4_be) and x^(4p) * H^(8 << t) (p4g_be[t]): 128, on the 192 lanes of waves 1-3
+      const int idx = 64 * (wave - 1) + lane;
+      if (idx < 128) {
+        const int set = idx >> 5, p = idx & 31;
+        uint32_t v[4];
+#pragma unroll
+        for (int w = 0; w < 4; w++) v[w] = set == 0 ? F[6][w] : set == 1 ? F[3][w] : set == 2 ? F[4][w] : F[5][w];
+        gf_mulxk(v, 4u * (uint32_t)p);
+        uint32_t* dst = set == 0 ? o->p4_be[p] : o->p4g_be[set - 1][p];
+        *reinterpret_cast<uint4*>(dst) = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    }
+    KS_STAMP(6);
+  } else {
+    // H^(lane+1): doubling scan, each level's products by a table of the level's one factor H^(2^k)
+    const uint32_t wb = (uint32_t)wave * kSetupTab;
 #pragma unroll 1
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y[4];
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t y[4];
 #pragma unroll
-    for (int w = 0; w < 4; w++) y[w] = (uint32_t)__builtin_amdgcn_readlane((int)P[w], d - 1);
-    wave_lds_sync();  // the previous level's table reads are done before the table is rebuilt
-    table_of(wb, y, lane);
-    wave_lds_sync();
-    uint32_t x[4];
-    const int src = lane >= d ? lane - d : lane;
+      for (int w = 0; w < 4; w++) y[w] = (uint32_t)__builtin_amdgcn_readlane((int)P[w], d - 1);
+      wave_lds_sync();  // the previous level's table reads are done before the table is rebuilt
+      table_of(wb, y, lane);
+      wave_lds_sync();
+      uint32_t x[4];
+      const int src = lane >= d ? lane - d : lane;
 #pragma unroll
-    for (int w = 0; w < 4; w++) x[w] = (uint32_t)__shfl((int)P[w], src, 64);
-    table_mul(x, wb);
-    if (lane >= d && lane < 2 * d) {
+      for (int w = 0; w < 4; w++) x[w] = (uint32_t)__shfl((int)P[w], src, 64);
+      table_mul(x, wb);
+      if (lane >= d && lane < 2 * d) {
 #pragma unroll
-      for (int w = 0; w < 4; w++) P[w] = x[w];
+        for (int w = 0; w < 4; w++) P[w] = x[w];
+      }
+      if (d == 1) KS_STAMP(5);
+    }
+    KS_STAMP(6);
+    *reinterpret_cast<uint4*>(o->hpow_be[lane]) = make_uint4(P[0], P[1], P[2], P[3]);
+    // record-table seeds: x^(4p) * H^64 (p4_be) and x^(4p) * H^(8 << t) (p4g_be[t]), 128 in all, 2 per lane
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int idx = lane + 64 * s, set = idx >> 5, p = idx & 31;
+      const int from = set == 0 ? 63 : (8 << (set - 1)) - 1;  // lane holding H^64, H^8, H^16, H^32
+      uint32_t v[4];
+#pragma unroll
+      for (int w = 0; w < 4; w++) v[w] = (uint32_t)__shfl((int)P[w], from, 64);
+      gf_mulxk(v, 4u * (uint32_t)p);
+      uint32_t* dst = set == 0 ? o->p4_be[p] : o->p4g_be[set - 1][p];
+      *reinterpret_cast<uint4*>(dst) = make_uint4(v[0], v[1], v[2], v[3]);
     }
   }
-  *reinterpret_cast<uint4*>(o->hpow_be[lane]) = make_uint4(P[0], P[1], P[2], P[3]);
-  // record-table seeds: x^(4p) * H^64 (p4_be) and x^(4p) * H^(8 << t) (p4g_be[t]), 128 in all, 2 per lane
-#pragma unroll
-  for (int s = 0; s < 2; s++) {
-    const int idx = lane + 64 * s, set = idx >> 5, p = idx & 31;
-    const int from = set == 0 ? 63 : (8 << (set - 1)) - 1;  // lane holding H^64, H^8, H^16, H^32
-    uint32_t v[4];
-#pragma unroll
-    for (int w = 0; w < 4; w++) v[w] = (uint32_t)__shfl((int)P[w], from, 64);
-    gf_mulxk(v, 4u * (uint32_t)p);
-    uint32_t* dst = set == 0 ? o->p4_be[p] : o->p4g_be[set - 1][p];
-    *reinterpret_cast<uint4*>(dst) = make_uint4(v[0], v[1], v[2], v[3]);
-  }
-  if (lane == 0) {
+  if (writer && lane == 0) {
     o->suite = suite;
     o->nr = nr;
     o->key_len = key_len;
     o->valid = 1u;
   }
+#ifdef ATLS_KS_STAMPS
+  KS_STAMP(7);
+  if (i_key == 0 && threadIdx.x == 0) atomicAdd(&g_ks_stamps[15], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 }  // namespace atls
@@ -249,19 +383,37 @@ extern "C" int atls_launch_build_t0(uint32_t* t0, hipStream_t s) {
 // keys: a device array of n keys, or (n <= atls_key_setup_inline_max()) nullptr with host_keys, whose
 // contents then travel in the kernel arguments (no copy, nothing to wait for before the call returns).
 extern "C" int atls_key_setup_inline_max(void) { return atls::kInlineKeys; }
+
+// Debug: copy out (and reset) the key installs' phase clocks of a -DATLS_KS_STAMPS build; -1 otherwise.
+extern "C" int atls_debug_ks_stamps(unsigned long long* out) {
+#ifdef ATLS_KS_STAMPS
+  unsigned long long h[16], z[16] = {};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(atls::g_ks_stamps), sizeof(h)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(atls::g_ks_stamps), z, sizeof(z)) != hipSuccess) return -1;
+  for (int i = 0; i < 16; i++) out[i] = h[i];
+  return 0;
+#else
+  (void)out;
+  return -1;
+#endif
+}
 extern "C" int atls_launch_key_setup(const atls_key* keys, const atls_key* host_keys, uint32_t n, void* ks,
-                                     hipStream_t s) {
+                                     const uint32_t* t0, hipStream_t s) {
   if (n == 0) return 0;
   atls::KeySetupArgs A{};
   A.keys = keys;
   A.n = n;
   A.ks = (atls::KeySched*)ks;
+  A.t0 = t0;
   if (!keys) {
     if (!host_keys || n > (uint32_t)atls::kInlineKeys) return ATLS_INTERNAL_ERROR;
     __builtin_memcpy(A.inl, host_keys, sizeof(atls_key) * n);
   }
   const uint32_t blocks = (n + atls::kSetupWaves - 1) / atls::kSetupWaves;
-  hipLaunchKernelGGL(atls::key_setup_kernel, dim3(blocks), dim3(64 * atls::kSetupWaves),
-                     atls::kSetupT0 + 1024, s, A);
+  if (n == 1 && ATLS_KS_ONE)  // one key: the whole workgroup on it (latency)
+    hipLaunchKernelGGL(atls::key_setup_kernel<true>, dim3(1), dim3(64 * atls::kSetupWaves), atls::kOneT0 + 1024, s, A);
+  else
+    hipLaunchKernelGGL(atls::key_setup_kernel<false>, dim3(blocks), dim3(64 * atls::kSetupWaves),
+                       atls::kSetupT0 + 1024, s, A);
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }

@@ -123,3 +123,20 @@ def test_many_keys_one_launch_match_model():
             assert not bad, (i, bad)
     finally:
         eng.close()
+
+
+def _square(v):
+    """keysetup.hip gf_square, restated on a Python int: coefficient x^i -> x^(2i) (bit b of each 64-bit
+    half -> bit 2b + 1), the high half's image O(x) folded back as O * (1 + x + x^2 + x^7)."""
+    def spread(x):
+        return sum(((x >> b) & 1) << (2 * b + 1) for b in range(64))
+
+    lo, hi = v >> 64, v & ((1 << 64) - 1)  # x^0..x^63 in the high 64 bits of the number
+    o = spread(hi)
+    return spread(lo) ^ o ^ _mulxk64(o, 1) ^ _mulxk64(o, 2) ^ _mulxk64(o, 7)
+
+
+def test_one_step_square_equals_product():
+    for _ in range(30):
+        v = int.from_bytes(RNG.integers(0, 256, 16, dtype=np.uint8).tobytes(), "big")
+        assert _square(v) == km.gf_mul(v, v)

@@ -91,6 +91,30 @@ int main() {
   printf("{\"empty_launch_sync_us\": %.1f, \"empty_launch_flag_spin_us\": %.1f, \"empty_launch_writevalue_spin_us\": %.1f, "
          "\"empty_launch_3712B_args_flag_spin_us\": %.1f",
          sync_us, spin_us, wv_us, big_us);
+  // (f) a new key: atls_update_keys of one AES-128 / AES-256 slot (key-setup kernel, the key in the launch
+  // arguments), then a wait on the engine stream -- the end-to-end cost of a connection's new key
+  for (int kl : {16, 32}) {
+    atls_engine* e = atls_engine_create(0);
+    if (!e) abort();
+    std::vector<atls_key> ks(64);
+    for (size_t i = 0; i < ks.size(); i++) {
+      memset(&ks[i], 0, sizeof ks[i]);
+      ks[i].suite = kl == 16 ? ATLS_TLS_AES_128_GCM_SHA256 : ATLS_TLS_AES_256_GCM_SHA384;
+      ks[i].key_len = (uint8_t)kl;
+      ks[i].iv_len = 12;
+      for (int b = 0; b < 32; b++) ks[i].key[b] = (uint8_t)(i * 31 + b);
+    }
+    if (atls_set_keys(e, ks.data(), (uint32_t)ks.size())) abort();
+    hipStream_t es = (hipStream_t)atls_engine_stream(e);
+    uint32_t slot = 0;
+    const double up = median_us([&] {
+      slot = (slot + 1) % 64;
+      if (atls_update_keys(e, slot, &ks[slot], 1)) abort();
+      (void)hipStreamSynchronize(es);
+    }, 2000);
+    printf("%s\"aes%d_update1_stream_sync_us\": %.1f", kl == 16 ? ", " : ", ", kl * 8, up);
+    atls_engine_destroy(e);
+  }
   std::vector<uint8_t> key(32, 7), iv(12, 1), aad = {0x17, 3, 3, 0x06, 0x11}, tag(16);
   for (uint16_t suite : {(uint16_t)ATLS_TLS_CHACHA20_POLY1305_SHA256, (uint16_t)ATLS_TLS_AES_128_GCM_SHA256}) {
     const size_t kl = suite == ATLS_TLS_AES_128_GCM_SHA256 ? 16 : 32;
