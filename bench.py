@@ -605,6 +605,15 @@ def main():
             mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join)
             cfgs[name] = config_summary(name, mm, steps)
             del mm
+        if world == 1 and not args.records:
+            # C4 at its stated size on one GPU: the whole 1 Mi x 16 KiB batch (17.2 GB in, 17.2 GB out) in one
+            # device-resident launch -- what the 8-GPU config's root holds before it scatters
+            name = "c4_aes256gcm_1Mi_x_16KiB"
+            mm = measure(name, eng, dev, rank, world, min(steps, 5), min(warmup, 1), not args.no_lazy_join,
+                         records=workload.CONFIGS[name][1])
+            cfgs[name + " (whole batch, 1 GPU)"] = config_summary(name, mm, min(steps, 5))
+            del mm
+            torch.cuda.empty_cache()
         if rank == 0:
             result["configs"] = cfgs
     if rank == 0:
