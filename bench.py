@@ -605,6 +605,13 @@ def main():
             mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join)
             cfgs[name] = config_summary(name, mm, steps)
             del mm
+        if not args.key_slots:
+            # SURVEY §8(d)'s worst case: C2 with a key per record (65,536 connections), so no lane groups form
+            name = "c2_aes128gcm_64Ki_x_16KiB"
+            mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join,
+                         key_slots=workload.CONFIGS[name][1])
+            cfgs[name + " (a key per record)"] = config_summary(name, mm, steps)
+            del mm
         if world == 1 and not args.records:
             # C4 at its stated size on one GPU: the whole 1 Mi x 16 KiB batch (17.2 GB in, 17.2 GB out) in one
             # device-resident launch -- what the 8-GPU config's root holds before it scatters
