@@ -134,20 +134,18 @@ struct atls_multi {
   // transfers are RCCL send / recv of rank 0 to itself on the root's transfer stream. The batch
   // then goes through exactly the RCCL branch of run_device on a one-GPU box (tests).
   bool rccl_self = false;
+  size_t xfer_chunk = ~size_t(0);  // largest RCCL message (multi_xfer_chunk() at creation)
   std::mutex mu;
 };
 
 namespace {
 
-// Largest RCCL point-to-point message (ATLS_MULTI_CHUNK_MB, default 1024 MiB; 0 = none): larger ranges go
-// in several messages.
+// Largest RCCL point-to-point message (ATLS_MULTI_CHUNK_MB when the multi engine is created, default
+// 1024 MiB; 0 = none): larger ranges go in several messages.
 size_t multi_xfer_chunk() {
-  static const size_t v = [] {
-    const char* e = std::getenv("ATLS_MULTI_CHUNK_MB");
-    const long mb = e ? std::atol(e) : 1024;
-    return mb > 0 ? (size_t)mb << 20 : ~size_t(0);
-  }();
-  return v;
+  const char* e = std::getenv("ATLS_MULTI_CHUNK_MB");
+  const long mb = e ? std::atol(e) : 1024;
+  return mb > 0 ? (size_t)mb << 20 : ~size_t(0);
 }
 
 // Wait for everything queued for this batch (engine streams, transfer streams), and clear the
@@ -220,7 +218,7 @@ int run_device(atls_multi* m, bool open, const atls_rec* recs, const uint32_t* f
       // sides: one C4 range is 2 GiB each way (131,072 x 16 KiB), and a single RCCL point-to-point
       // message of 2^31 bytes or more came back wrong on the one-GPU self exchange
       // (tests/test_gpu_c4_full.py, round 4).
-      const size_t piece = multi_xfer_chunk();
+      const size_t piece = m->xfer_chunk;
       auto send = [&](const void* p, size_t bytes, int peer, ncclComm_t c, hipStream_t st) {
         for (size_t o = 0; o < bytes; o += piece)
           chk(R.send((const uint8_t*)p + o, std::min(piece, bytes - o), ncclUint8, peer, c, st));
@@ -471,6 +469,7 @@ atls_multi* atls_multi_create(const int* devices, int n_devices) {
     }
     m->use_rccl = true;
     m->rccl_self = self;
+    m->xfer_chunk = multi_xfer_chunk();
   }
   return m;
 }

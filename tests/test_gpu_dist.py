@@ -45,14 +45,19 @@ def _single_seal(b, inbuf, recs=None, out_bytes=None):
     return out, tags
 
 
-@pytest.mark.parametrize("devices,rccl_self", [([0], False), ([0, 0], False), ([0, 0, 0], False), ([0, 0], True),
-                                               ([0, 0, 0, 0], True)],
-                         ids=["1-copy", "2-copy", "3-copy", "2-rccl-self", "4-rccl-self"])
-def test_multi_engine_device_buffers_equal_single_engine(devices, rccl_self, monkeypatch):
+@pytest.mark.parametrize("devices,rccl_self,chunk_mb", [([0], False, None), ([0, 0], False, None), ([0, 0, 0], False, None),
+                                                        ([0, 0], True, None), ([0, 0, 0, 0], True, None),
+                                                        ([0, 0, 0], True, "1")],
+                         ids=["1-copy", "2-copy", "3-copy", "2-rccl-self", "4-rccl-self", "3-rccl-self-1MiB-pieces"])
+def test_multi_engine_device_buffers_equal_single_engine(devices, rccl_self, chunk_mb, monkeypatch):
+    """...; with ATLS_MULTI_CHUNK_MB=1 every range travels in several RCCL messages (the 1 GiB cap of
+    csrc/multi.cpp scaled down), matched in order on both sides."""
     b, inbuf = _batch()
     ref_out, ref_tags = _single_seal(b, inbuf)
     if rccl_self:
         monkeypatch.setenv("ATLS_MULTI_RCCL_SELF", "1")
+    if chunk_mb:
+        monkeypatch.setenv("ATLS_MULTI_CHUNK_MB", chunk_mb)
     m = atls.MultiEngine(devices)
     assert m.uses_rccl == rccl_self  # repeated device: copies, or RCCL rank 0 to itself
     m.set_keys(b["keys"])
