@@ -54,6 +54,9 @@ namespace atls {
 #define ATLS_GCM_FAST_FIRST 0  // 1: a TLS record's first step (E_K(J0), AAD, 62 data blocks) without the general step's
                                // classification, when it holds 62 whole blocks (round 4 A/B on C5)
 #endif
+#ifndef ATLS_SINGLE_FAST_FIRST
+#define ATLS_SINGLE_FAST_FIRST 1  // the same in the single-call kernel (gcm_single: one wave's latency, no occupancy)
+#endif
 #ifndef ATLS_PREFETCH
 #define ATLS_PREFETCH 1  // fast steps load the next step's data block before their own AES rounds
 #endif
@@ -75,6 +78,20 @@ namespace atls {
 constexpr int kTabBytes = 65536;
 constexpr int kGhashBytes = 8192;
 constexpr size_t lds_bytes(int waves) { return kTabBytes + (size_t)(ATLS_DBG_SHARED_GHASH ? 1 : waves) * kGhashBytes; }
+
+// The lane combine's product Y_l * H^e_l of gcm_record (gcm_common.h): through the wave's GHASH table
+// region, except in the shared-table timing build where other waves still read it.
+// AES-256 batches keep the register comb: the LDS form measured 1.3 % slower on C4 (its records mostly take
+// the lane-group kernel, whose code the change still reaches); the single call (LAT) takes the LDS form.
+#ifndef ATLS_COMB_AES256
+#define ATLS_COMB_AES256 0
+#endif
+template <int NR, bool LAT>
+__device__ __forceinline__ void lane_comb(const uint32_t (&yb)[4], const uint32_t (&hp)[4], uint32_t (&z)[4],
+                                          uint32_t wb, int lane) {
+  if (ATLS_COMB_LDS && !ATLS_DBG_SHARED_GHASH && (LAT || NR != 14 || ATLS_COMB_AES256)) gf_mul_comb_lds<ATLS_COMB_LDS == 2 ? 2 : 1>(yb, hp, z, wb, lane);
+  else gf_mul_comb(yb, hp, z);
+}
 
 template <int W>
 __device__ __forceinline__ void ghash_mul(uint32_t (&y)[4], uint32_t wb) {
@@ -294,7 +311,9 @@ __device__ unsigned long long g_tt_stamps[8];
 #define TT_STAMP(var)
 #endif
 
-template <int NR, bool OPEN>
+// LAT: the single-call kernel's record (one wave's latency, no occupancy to keep): the branch-free first
+// step (ATLS_SINGLE_FAST_FIRST) and the LDS lane combine at every key size.
+template <int NR, bool OPEN, bool LAT = false>
 __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx,
                            uint32_t lb, uint32_t wb, int lane) {
   TT_STAMP(t_start);
@@ -431,7 +450,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   uint4 Pn = make_uint4(0u, 0u, 0u, 0u);
   bool pref = false;
   const uint32_t lim = min(in_bytes, n_aead);
-  const bool first_fast = ATLS_GCM_FAST_FIRST && use_cache && tls && !(OPEN && wire) && fast_end >= 64u;
+  const bool first_fast = (LAT ? ATLS_SINGLE_FAST_FIRST : ATLS_GCM_FAST_FIRST) && use_cache && !(OPEN && wire) && fast_end >= 64u;  // TLS / WIRE / RAW (one AAD block)
   TT_STAMP(t_setup);
   for (uint32_t base = 0; base < S; base += 64) {
     TT_STAMP(t_step);
@@ -466,7 +485,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 #endif
       continue;
     }
-    if (ATLS_GCM_FAST_FIRST && base == 0u && first_fast) {
+    if ((LAT ? ATLS_SINGLE_FAST_FIRST : ATLS_GCM_FAST_FIRST) && base == 0u && first_fast) {
       // The first step without classification (round 4 A/B): lane 0 E_K(J0) (counter 1),
       // lane 1 the TLS AAD block, lanes 2..63 data blocks 0..61 (counters 2..63) -- whole blocks when
       // the record has at least 62 of them. Same counter cache as the fast steps (ctr >> 8 = 0).
@@ -482,12 +501,24 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       aes_cached(st, ((lo << 8) | lb) ^ (k15 << 8), 0u);
       const v4u32 C = {Pu.x ^ st[0], Pu.y ^ st[1], Pu.z ^ st[2], Pu.w ^ st[3]};
       if (lane >= 2) st16(dst + off, make_uint4(C.x, C.y, C.z, C.w));
-      if (OPEN && lane >= 2) lastnz = block_last_nz(C.x, C.y, C.z, C.w, off, lastnz);
+      if (OPEN && tls && lane >= 2) lastnz = block_last_nz(C.x, C.y, C.z, C.w, off, lastnz);
       if (lane == 0) { e0 = st[0]; e1 = st[1]; e2 = st[2]; e3 = st[3]; }
-      if (lane == 1) { y[0] = hdr0; y[1] = hdr1; }  // Y = 0 before the first step: Y = B
+      if (lane == 1) {  // Y = 0 before the first step: Y = B, the AAD block
+        if (tls) {
+          y[0] = hdr0; y[1] = hdr1;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 16; q++)
+            if ((uint32_t)q < aad_len) put_byte(y, q, aadp[q]);
+        }
+      }
       if (lane >= 2) {
         y[0] = OPEN ? Pu.x : C.x; y[1] = OPEN ? Pu.y : C.y; y[2] = OPEN ? Pu.z : C.z; y[3] = OPEN ? Pu.w : C.w;
       }
+#ifdef ATLS_TT_STAMPS
+      t_fast += __builtin_amdgcn_s_memtime() - t_step;  // counted with the fast steps
+      n_fast++;
+#endif
       continue;
     }
     pref = false;
@@ -600,7 +631,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   uint32_t z[4] = {0, 0, 0, 0};
   if (s_last >= 1) {
     const uint32_t yb[4] = {bswap32(y[0]), bswap32(y[1]), bswap32(y[2]), bswap32(y[3])};
-    gf_mul_comb(yb, hp, z);
+    lane_comb<NR, LAT>(yb, hp, z, wb, lane);
   }
 #pragma unroll
   for (int w = 0; w < 4; w++) z[w] = wave_xor(z[w]);
@@ -935,7 +966,7 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
 }
 
 // One record by the whole wave (gcm_record), after the direct-mode descriptor check.
-template <int NR, bool OPEN>
+template <int NR, bool OPEN, bool LAT = false>
 __device__ __forceinline__ void gcm_one(const GcmArgs& A, uint32_t r, uint32_t lb, uint32_t wb, int lane) {
   {
     atls_rec d = A.recs[r];
@@ -955,7 +986,7 @@ __device__ __forceinline__ void gcm_one(const GcmArgs& A, uint32_t r, uint32_t l
         return;
       }
     }
-    gcm_record<NR, OPEN>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
+    gcm_record<NR, OPEN, LAT>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
     wave_lds_sync();  // table reads of this record done before the next record rebuilds it
   }
 }
@@ -1067,7 +1098,7 @@ __global__ __launch_bounds__(64 * kSingleWaves) void gcm_single(GcmSingle) {
   __syncthreads();
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x & 63;
-  gcm_one<NR, OPEN>(A, 0u, 4u * (uint32_t)(lane & 31), (uint32_t)kTabBytes, lane);
+  gcm_one<NR, OPEN, true>(A, 0u, 4u * (uint32_t)(lane & 31), (uint32_t)kTabBytes, lane);
   signal_done(A.done, A.done_val, lane);
 }
 

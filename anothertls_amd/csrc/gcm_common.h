@@ -162,6 +162,78 @@ __device__ __forceinline__ void gf_mul_comb(const uint32_t (&x)[4], const uint32
   z[0] = z0; z[1] = z1; z[2] = z2; z[3] = z3;
 }
 
+// The same product through per-lane tables in the LDS at tb (the wave's 8 KiB GHASH table, whose
+// last product has been read by then: a wave's LDS operations run in order), lane l's entry n at
+// tb + n*1024 + l*16 (a ds_read_b128 lane group's 16 lanes hit 16 different bank quads whatever n
+// each reads). The lookups do not depend on z, so they issue ahead of the Horner chain.
+//   MODE 1: entry n (0..7) = XOR of Q_w over the set bits w of n; one lookup serves words 0-2 of
+//           x, word 3 keeps its masked XORs: 45 -> 25 VALU instructions per j.
+//   MODE 2: entries 0..3 from (Q_0, Q_1), 4..7 from (Q_2, Q_3); two lookups per j, no masked XORs:
+//           ~20 VALU instructions and twice the LDS reads.
+// ATLS_COMB_LDS picks the mode for gcm_record (0 = gf_mul_comb); the lane-group kernel keeps
+// gf_mul_comb, where the LDS form measured no faster (C2) or 1 % slower (C4).
+#ifndef ATLS_COMB_LDS
+#define ATLS_COMB_LDS 1
+#endif
+#ifndef ATLS_COMB_UNROLL
+#define ATLS_COMB_UNROLL 4
+#endif
+template <int MODE>
+__device__ __forceinline__ void gf_mul_comb_lds(const uint32_t (&x)[4], const uint32_t (&p)[4], uint32_t (&z)[4],
+                                                uint32_t tb, int lane) {
+  uint32_t q[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) q[0][c] = p[c];
+#pragma unroll
+  for (int t = 1; t < 4; t++) {
+    const uint32_t w = q[t - 1][3];
+    q[t][0] = w ^ (w >> 1) ^ (w >> 2) ^ (w >> 7);
+    q[t][1] = q[t - 1][0] ^ (w << 31) ^ (w << 30) ^ (w << 25);
+    q[t][2] = q[t - 1][1];
+    q[t][3] = q[t - 1][2];
+  }
+  const uint32_t la = tb + (uint32_t)lane * 16u;
+#pragma unroll
+  for (int n = 0; n < 8; n++) {
+    v4u32 e;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      if (MODE == 1) e[c] = ((n & 1) ? q[0][c] : 0u) ^ ((n & 2) ? q[1][c] : 0u) ^ ((n & 4) ? q[2][c] : 0u);
+      else e[c] = ((n & 1) ? q[(n >> 2) * 2][c] : 0u) ^ ((n & 2) ? q[(n >> 2) * 2 + 1][c] : 0u);
+    }
+    *reinterpret_cast<__attribute__((address_space(3))) v4u32*>(la + (uint32_t)n * 1024u) = e;
+  }
+  uint32_t z0 = 0, z1 = 0, z2 = 0, z3 = 0;
+#pragma unroll ATLS_COMB_UNROLL
+  for (int j = 31; j >= 0; j--) {
+    const uint32_t b = 31u - (uint32_t)j;  // c(32w + j) = bit b of x[w]
+    const uint32_t r = (uint32_t)__builtin_amdgcn_sbfe((int)z3, 0, 1) & 0xE1000000u;  // z <- z * X
+    const uint32_t s3 = __builtin_amdgcn_alignbit(z2, z3, 1);
+    const uint32_t s2 = __builtin_amdgcn_alignbit(z1, z2, 1);
+    const uint32_t s1 = __builtin_amdgcn_alignbit(z0, z1, 1);
+    const uint32_t s0 = z0 >> 1;
+    if (MODE == 1) {
+      const uint32_t idx = __builtin_amdgcn_ubfe(x[0], b, 1) | (__builtin_amdgcn_ubfe(x[1], b, 1) << 1) |
+                           (__builtin_amdgcn_ubfe(x[2], b, 1) << 2);
+      const v4u32 t = lds_u4(la + (idx << 10));
+      const uint32_t m = (uint32_t)__builtin_amdgcn_sbfe((int)x[3], b, 1);
+      z0 = xor3(s0, r, t.x ^ (m & q[3][0]));
+      z1 = xor3(s1, t.y, m & q[3][1]);
+      z2 = xor3(s2, t.z, m & q[3][2]);
+      z3 = xor3(s3, t.w, m & q[3][3]);
+    } else {
+      const uint32_t ia = __builtin_amdgcn_ubfe(x[0], b, 1) | (__builtin_amdgcn_ubfe(x[1], b, 1) << 1);
+      const uint32_t ib = __builtin_amdgcn_ubfe(x[2], b, 1) | (__builtin_amdgcn_ubfe(x[3], b, 1) << 1);
+      const v4u32 ta = lds_u4(la + (ia << 10)), tb4 = lds_u4(la + 4096u + (ib << 10));
+      z0 = xor3(s0, r, ta.x) ^ tb4.x;
+      z1 = xor3(s1, ta.y, tb4.y);
+      z2 = xor3(s2, ta.z, tb4.z);
+      z3 = xor3(s3, ta.w, tb4.w);
+    }
+  }
+  z[0] = z0; z[1] = z1; z[2] = z2; z[3] = z3;
+}
+
 // XOR of x over the wave without the LDS (ds_bpermute) path of __shfl_xor: four DPP steps leave
 // every lane with its 16-lane row's XOR (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
 // row_mirror), then four v_readlane combine the rows. Wave-uniform result.

@@ -141,3 +141,24 @@ def test_argument_block_boundary_vs_oracle(suite, klen):
                 with pytest.raises(atls.TlsError) as e:
                     c.decrypt(key, iv, ct, aad, tag[:15] + bytes([tag[15] ^ 0x80]))
                 assert e.value.code == 20
+
+
+@pytest.mark.parametrize("suite,klen", [(0x1301, 16), (0x1302, 32)])
+def test_single_first_step_boundary_vs_oracle(suite, klen):
+    """The single-call kernel's branch-free first step (gcm.hip ATLS_SINGLE_FAST_FIRST: lane 0 E_K(J0),
+    lane 1 the AAD block, lanes 2-63 data) takes records with one AAD block (1..16 B), a 96-bit IV and at
+    least 62 whole data blocks; both sides of that boundary, seal and open, against the oracle."""
+    rng = random.Random(klen * 13 + suite)
+    key = bytes(rng.getrandbits(8) for _ in range(klen))
+    c = atls.CipherSuite(suite).get_cipher()
+    for aad_len in (0, 1, 5, 13, 16, 17):
+        for n in (975, 991, 992, 993, 1008, 1009, 1024, 2047, 3000):
+            iv = bytes(rng.getrandbits(8) for _ in range(12))
+            aad = bytes(rng.getrandbits(8) for _ in range(aad_len))
+            pt = bytes(rng.getrandbits(8) for _ in range(n))
+            ct, tag = c.encrypt(key, iv, pt, aad)
+            rc, ect, etag = ora.cipher_encrypt(suite, key, iv, pt, aad)
+            assert rc == 0 and ct == ect and tag == etag, (aad_len, n)
+            assert c.decrypt(key, iv, ct, aad, tag) == pt
+            with pytest.raises(atls.TlsError):
+                c.decrypt(key, iv, ct, aad, bytes([tag[0] ^ 1]) + tag[1:])

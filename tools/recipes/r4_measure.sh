@@ -28,3 +28,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_keysetup -o run --
 timeout -k 10 120 ./tools/single_call_floor > $O/single_call_floor.json 2>&1 || exit 1
 timeout -k 10 300 python3 tools/single_call_latency.py > $O/single_call_latency.json 2>&1 || exit 1
 cat $O/bench_default.json $O/single_call_floor.json
+ATLS_LIB=$PWD/anothertls_amd/variants/libatls_ttstamps.so timeout -k 10 180 python3 tools/tt_stamps_single.py > $O/gcm_single_stamps.json 2>&1 || { cat $O/gcm_single_stamps.json; exit 1; }
+cat $O/single_call_latency.json $O/gcm_single_stamps.json
