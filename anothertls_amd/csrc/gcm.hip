@@ -54,6 +54,9 @@ namespace atls {
 #define ATLS_GCM_FAST_FIRST 0  // 1: a TLS record's first step (E_K(J0), AAD, 62 data blocks) without the general step's
                                // classification, when it holds 62 whole blocks (round 4 A/B on C5)
 #endif
+#ifndef ATLS_GCM_SPREAD
+#define ATLS_GCM_SPREAD 1  // planned batches: work-list rows spread over the workgroups, odd rows reversed (gcm_kernel)
+#endif
 #ifndef ATLS_SINGLE_FAST_FIRST
 #define ATLS_SINGLE_FAST_FIRST 1  // the same in the single-call kernel (gcm_single: one wave's latency, no occupancy)
 #endif
@@ -994,7 +997,7 @@ __device__ __forceinline__ void gcm_one(const GcmArgs& A, uint32_t r, uint32_t l
 // WAVES waves per workgroup (one record per wave at a time), one workgroup per CU: the LDS
 // footprint (64 KiB tables + 8 KiB per wave) is what limits residency. One launch per AES round
 // count (a kernel holds only that count's round keys); the waves take the records of that round
-// count's work list (plan.hip, longest first) round-robin, or a key-grouped direct batch's lane
+// count's work list (plan.hip, longest first) round-robin, spread over the workgroups, or a key-grouped direct batch's lane
 // groups from a work counter.
 template <bool OPEN, int kWaves, int NR>
 __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
@@ -1013,9 +1016,19 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
   const uint32_t wb = (uint32_t)kTabBytes + (ATLS_DBG_SHARED_GHASH ? 0u : (uint32_t)wave * kGhashBytes);
   const WorkList W{A.idx, A.plan, NR == 10 ? kListGcm10 : NR == 12 ? kListGcm12 : kListGcm14, A.n};
   const uint32_t stride = gridDim.x * kWaves;
-  if (!A.gidx) {  // one record per wave, positions of the work list round-robin
+  if (!A.gidx) {  // one record per wave
+    // The work list runs longest first, `stride` positions per row. Row-major round-robin gave
+    // workgroup b (one per CU) the 12 adjacent positions 12b..12b+11 of every row, i.e. CU 0 the
+    // longest records of each row: on C5's AES records the busiest CU carried 1.18x the mean CU load.
+    // Position p of a row goes to wave p / gridDim.x of workgroup p % gridDim.x (every CU samples the
+    // whole row), and odd rows run backwards (the waves that took long records take short ones next):
+    // 1.01x (simulated on the C5 shard).
     const uint32_t cnt = uni(W.size());
-    for (uint32_t q = blockIdx.x * kWaves + wave; q < cnt; q += stride) gcm_one<NR, OPEN>(A, uni(W.record(q)), lb, wb, lane);
+    const uint32_t p = ATLS_GCM_SPREAD ? (uint32_t)wave * gridDim.x + blockIdx.x : blockIdx.x * kWaves + wave;
+    for (uint32_t row = 0; row * stride < cnt; row++) {
+      const uint32_t q = row * stride + ((ATLS_GCM_SPREAD && (row & 1u)) ? stride - 1u - p : p);
+      if (q < cnt) gcm_one<NR, OPEN>(A, uni(W.record(q)), lb, wb, lane);
+    }
     if (A.done && cnt == 1u && blockIdx.x == 0 && wave == 0) signal_done(A.done, A.done_val, lane);
     return;
   }

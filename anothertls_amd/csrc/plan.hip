@@ -12,8 +12,9 @@
 //     C5 batch; ATLS_PLAN_FUSED_SCAN=0 restores it.)
 //
 // The record kernels (gcm.hip, chacha.hip) take their list's positions round-robin (WorkList,
-// plan.h), so every worker gets a similar mix of lengths (LPT-like balance for the
-// variable-length batches of BASELINE config C5).
+// plan.h) -- AES-GCM with each row spread over the workgroups and odd rows reversed, ChaCha in
+// 16-record workgroups dispatched longest first -- so every CU gets a similar mix of lengths
+// (LPT-like balance for the variable-length batches of BASELINE config C5).
 #include "plan.h"
 
 namespace atls {
