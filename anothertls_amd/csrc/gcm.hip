@@ -306,12 +306,24 @@ __device__ __forceinline__ void aes_ctr_r12(uint32_t (&s)[4], uint32_t addr1, co
 
 // Phase timing (build with -DATLS_TT_STAMPS): shader-clock totals over all records, read back with
 // atls_debug_tt_stamps(). 0 setup (tables, counter cache), 1 fast steps, 2 general steps,
-// 3 lane combine + tag, 4 records, 5 fast steps, 6 general steps.
+// 3 lane combine + tag, 4 records, 5 fast steps, 6 general steps; general steps split: 8 the first step's
+// cycles, 9 the later ones', 10 until their data loads landed, 11 their AES, 12 first steps counted.
 #ifdef ATLS_TT_STAMPS
-__device__ unsigned long long g_tt_stamps[8];
+__device__ unsigned long long g_tt_stamps[16];
 #define TT_STAMP(var) const uint64_t var = __builtin_amdgcn_s_memtime()
 #else
 #define TT_STAMP(var)
+#endif
+
+// The last (general) step of a record without loads of its own (ATLS_GEN_PN, round 4 A/B, off): a wave's
+// vector-memory counter counts its stores too and drains in order, so a load issued after the fast steps'
+// stores waits for all of them (tools/tt_stamps.py: a C5 record's last step took 13x a fast step's wave
+// time). The fast step before it already loads the general step's whole blocks (Pn); with the switch the
+// lane whose block is partial loads the input's last 16 bytes instead of a dummy and the general step
+// takes both from Pn. The step's wave time falls 2.8x (C5) but the launch does not get shorter (the other
+// waves were covering the wait) and the open kernel gets 8 % slower (registers): DESIGN §4.2.
+#ifndef ATLS_GEN_PN
+#define ATLS_GEN_PN 0
 #endif
 
 // LAT: the single-call kernel's record (one wave's latency, no occupancy to keep): the branch-free first
@@ -321,7 +333,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
                            uint32_t lb, uint32_t wb, int lane) {
   TT_STAMP(t_start);
 #ifdef ATLS_TT_STAMPS
-  uint64_t t_fast = 0, t_gen = 0, n_fast = 0, n_gen = 0;
+  uint64_t t_fast = 0, t_gen = 0, n_fast = 0, n_gen = 0, t_gen0 = 0, t_genl = 0, t_ld = 0, t_aes = 0, n_gen0 = 0;
 #endif
   uint32_t rk[4 * (NR + 1)], rkr[4 * (NR + 1)];
 #pragma unroll
@@ -451,7 +463,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   // (1 KiB further) before its own AES rounds, so the HBM latency hides under a whole step instead
   // of the last rounds; `pref` (wave-uniform) says Pn holds this step's block.
   uint4 Pn = make_uint4(0u, 0u, 0u, 0u);
-  bool pref = false;
+  bool pref = false, gen_pn = false;
   const uint32_t lim = min(in_bytes, n_aead);
   const bool first_fast = (LAT ? ATLS_SINGLE_FAST_FIRST : ATLS_GCM_FAST_FIRST) && use_cache && !(OPEN && wire) && fast_end >= 64u;  // TLS / WIRE / RAW (one AAD block)
   TT_STAMP(t_setup);
@@ -464,7 +476,8 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       if (ATLS_PREFETCH) {  // every lane of a fast next step holds a whole block (fast_end)
         const uint32_t offn = off + 1024u;
         pref = base + 128u <= fast_end;
-        Pn = ld16(src + (offn + 16u <= lim ? offn : off));  // always issued (see pf_off)
+        gen_pn = ATLS_GEN_PN && !pref;  // the next step is a general one: its blocks come from Pn too
+        Pn = ld16(src + (offn + 16u <= lim ? offn : (ATLS_GEN_PN && offn < lim && lim >= 16u) ? lim - 16u : off));
       }
       const v4u32 P = {Pu.x, Pu.y, Pu.z, Pu.w};
       uint32_t st[4];
@@ -525,6 +538,8 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       continue;
     }
     pref = false;
+    const bool use_pn = gen_pn;  // this general step follows a fast step that loaded its blocks
+    gen_pn = false;
     if (ATLS_DBG_SKIP & 2) continue;
     if ((ATLS_DBG_SKIP & 16) && base + 64u >= S) continue;
     if ((ATLS_DBG_SKIP & 32) && base == 0u) continue;
@@ -547,7 +562,26 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     const uint32_t g = s - 1;
     if (s >= 1 && s <= m && g >= na && g < na + nb) {
       const uint32_t off = (g - na) * 16;
-      if (off + 16 <= in_bytes && (ATLS_GEN_VEC || src_al)) {
+      if (use_pn) {
+        // Pn holds this block (off + 16 <= lim) or the input's last 16 bytes (off < lim): shift the block's
+        // nv = lim - off bytes down from byte 16 - nv; past the input only the TLS content type (record.rs:173)
+        const uint32_t t[4] = {Pn.x, Pn.y, Pn.z, Pn.w};
+        if (off + 16u <= lim) {
+          P[0] = t[0]; P[1] = t[1]; P[2] = t[2]; P[3] = t[3];
+        } else {
+          const uint32_t nv = off < lim ? lim - off : 0u, sh = 16u - nv, ws = sh >> 2, bs = sh & 3u;
+          auto wd = [&](uint32_t i) { return i == 0 ? t[0] : i == 1 ? t[1] : i == 2 ? t[2] : i == 3 ? t[3] : 0u; };
+#pragma unroll
+          for (int w = 0; w < 4; w++) {
+            uint32_t v = __builtin_amdgcn_alignbyte(wd((uint32_t)w + ws + 1u), wd((uint32_t)w + ws), bs);
+            const int lo = 4 * w;
+            if ((int)nv < lo + 4) v &= ((int)nv <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - (int)nv)));
+            P[w] = nv ? v : 0u;
+          }
+          const uint32_t valid = min(16u, n_aead - off);
+          if (nv < valid) P[nv >> 2] |= (uint32_t)d.content_type << (8 * (nv & 3u));
+        }
+      } else if (off + 16 <= in_bytes && (ATLS_GEN_VEC || src_al)) {
         const uint4 v = ATLS_GEN_VEC ? ld16(src + off) : *reinterpret_cast<const uint4*>(src + off);
         P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
       } else {
@@ -561,6 +595,11 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
         }
       }
     }
+#ifdef ATLS_TT_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // timing build: the step's loads landed
+    const uint64_t t_l = __builtin_amdgcn_s_memtime();
+    t_ld += t_l - t_step;
+#endif
     if (use_cache) {  // ctr = 1 for slots 0..na, else 1 + s - na: the step's ctr >> 8 is lane 63's
       const uint32_t ctr = cb[3];
       const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)ctr, 63) >> 8;
@@ -568,6 +607,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     } else {
       aes_encrypt_tt<NR>(st, rk, rkr, lb);
     }
+#ifdef ATLS_TT_STAMPS
+    asm volatile("" ::"v"(st[0]), "v"(st[1]), "v"(st[2]), "v"(st[3]));
+    t_aes += __builtin_amdgcn_s_memtime() - t_l;
+#endif
     if (s == 0) { e0 = st[0]; e1 = st[1]; e2 = st[2]; e3 = st[3]; }
     uint32_t B[4] = {0, 0, 0, 0};
     if (s >= 1 && s <= m) {
@@ -624,8 +667,12 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       for (int w = 0; w < 4; w++) y[w] = yn[w] ^ B[w];
     }
 #ifdef ATLS_TT_STAMPS
-    t_gen += __builtin_amdgcn_s_memtime() - t_step;
-    n_gen++;
+    {
+      const uint64_t dt = __builtin_amdgcn_s_memtime() - t_step;
+      t_gen += dt;
+      n_gen++;
+      if (base == 0) { t_gen0 += dt; n_gen0++; } else t_genl += dt;
+    }
 #endif
   }
   TT_STAMP(t_loop);
@@ -673,6 +720,11 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     atomicAdd(&g_tt_stamps[4], 1ull);
     atomicAdd(&g_tt_stamps[5], (unsigned long long)n_fast);
     atomicAdd(&g_tt_stamps[6], (unsigned long long)n_gen);
+    atomicAdd(&g_tt_stamps[8], (unsigned long long)t_gen0);
+    atomicAdd(&g_tt_stamps[9], (unsigned long long)t_genl);
+    atomicAdd(&g_tt_stamps[10], (unsigned long long)t_ld);
+    atomicAdd(&g_tt_stamps[11], (unsigned long long)t_aes);
+    atomicAdd(&g_tt_stamps[12], (unsigned long long)n_gen0);
   }
 #endif
 }
@@ -1202,10 +1254,10 @@ extern "C" unsigned atls_build_flags(void) {
 // Debug: copy out (and reset) the phase timers of a -DATLS_TT_STAMPS build; -1 otherwise.
 extern "C" int atls_debug_tt_stamps(unsigned long long* out) {
 #ifdef ATLS_TT_STAMPS
-  unsigned long long h[8], z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long h[16], z[16] = {};
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(atls::g_tt_stamps), sizeof(h)) != hipSuccess) return -1;
   if (hipMemcpyToSymbol(HIP_SYMBOL(atls::g_tt_stamps), z, sizeof(z)) != hipSuccess) return -1;
-  for (int i = 0; i < 8; i++) out[i] = h[i];
+  for (int i = 0; i < 16; i++) out[i] = h[i];
   return 0;
 #else
   (void)out;

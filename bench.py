@@ -71,6 +71,12 @@ def parse():
     p.add_argument("--no-configs", action="store_true",
                    help="skip the other BASELINE configs (C3, C4 shard, C5 shard) timed after the headline one")
     p.add_argument("--config-steps", type=int, default=10, help="timed steps of each of those configs")
+    p.add_argument("--settle-ms", type=float, default=200.0,
+                   help="before the warm-up steps, time the on-device copy rate for this long (it also brings the "
+                        "GPU's clock up from idle, which a few 1-ms warm-up steps do not; 0 = after the steps)")
+    p.add_argument("--sustain-s", type=float, default=5.0,
+                   help="after the timed steps, seal the headline batch back to back for this long (every rank) "
+                        "and report the sustained rate (clocks under continuous load); 0 = skip")
     p.add_argument("--dry-run-cap", type=int, default=64,
                    help="--dry-run: content bytes per record of the whole-batch exchange rehearsal")
     p.add_argument("--dry-run", action="store_true",
@@ -322,11 +328,36 @@ def open_descs(recs):
 EXTRA_CONFIGS = ("c3_chacha20poly1305_64Ki_x_1.5KiB", "c4_aes256gcm_1Mi_x_16KiB", "c5_mixed_256Ki_x_64B-16KiB")
 
 
-def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_slots=None, keep=False):
+def copy_probe(d_in, d_out, min_ms):
+    """On-device copy rate (read + write GB/s) of this batch's buffers, d_in -> d_out, repeated for at
+    least min_ms of GPU time. Run before the warm-up steps it also takes the GPU out of its idle clock
+    state: MI355X's clock ramps over ~25 ms of load, longer than a few warm-up steps."""
+    nbytes = min(d_in.numel(), d_out.numel())
+    src, dst = d_in[:nbytes], d_out[:nbytes]
+    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    dst.copy_(src)
+    torch.cuda.synchronize()
+    reps, total_ms = 0, 0.0
+    c0.record()
+    while True:
+        for _ in range(10):
+            dst.copy_(src)
+        reps += 10
+        c1.record()
+        c1.synchronize()
+        total_ms = c0.elapsed_time(c1)
+        if total_ms >= min_ms:
+            break
+    return 2 * nbytes * reps / (total_ms * 1e-3) / 1e9
+
+
+def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_slots=None, keep=False,
+            settle_ms=0.0):
     """This rank's shard of config `name`, device-resident: `steps` timed seals (barrier + sync on both
     sides, max over ranks) with the kernels' interval from HIP events on the engine stream, then as many
     opens of the sealed records with every status, length and (uniform configs) plaintext byte checked.
-    Returns the numbers (and with keep=True the batch and its device buffers)."""
+    settle_ms > 0: the copy probe (copy_probe) runs that long first. Returns the numbers (and with
+    keep=True the batch and its device buffers)."""
     import anothertls_amd as atls
     from anothertls_amd import dist, workload
 
@@ -341,6 +372,7 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
     d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
     d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
     torch.cuda.synchronize(dev)
+    copy_gbps = copy_probe(d_in, d_out, settle_ms) if settle_ms > 0 else None
     # LAZY_JOIN: a mixed batch's ChaCha20-Poly1305 kernel is not joined back at the end of each step,
     # so the next step's plan and AES-GCM kernel start beside it (C5); no effect on one-suite batches
     flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC | (atls.FLAG_LAZY_JOIN if lazy else 0)
@@ -374,7 +406,7 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     m = {"batch": batch, "n": n, "wall": wall, "kern_ms": kern_ms, "payload": payload, "alg_bytes": alg_bytes,
          "achieved": achieved, "value": dist.whole_job_rate(payload, steps, wall, world), "flags": flags,
-         "stream": stream, "sync": sync}
+         "stream": stream, "sync": sync, "copy_gbps": copy_gbps}
 
     # ---- the decrypt half (Gcm::decrypt, gcm.rs:142-157, via record.rs:201-240) over the records
     # just sealed: same records, same bytes per record (read L + 16-byte tag, write L) ----
@@ -465,22 +497,35 @@ def main():
     eng = atls.Engine(local)
     # this rank's shard of the config's record stream (weak scaling: fixed records per GPU)
     m = measure(args.config, eng, dev, rank, world, args.steps, args.warmup, not args.no_lazy_join,
-                records=args.records, key_slots=args.key_slots, keep=True)
+                records=args.records, key_slots=args.key_slots, keep=True, settle_ms=args.settle_ms)
     batch, recs, n, payload = m["batch"], m["batch"]["recs"], m["n"], m["payload"]
     d_in, d_out, d_tags, d_aux = m["d_in"], m["d_out"], m["d_tags"], m["d_aux"]
     flags, stream, sync, kern_ms, achieved, alg_bytes = m["flags"], m["stream"], m["sync"], m["kern_ms"], m["achieved"], m["alg_bytes"]
 
-    # measured on-device copy bandwidth: read + write of this batch's payload buffer
-    d_cp = torch.empty_like(d_in)
-    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    d_cp.copy_(d_in)
-    c0.record()
-    for _ in range(10):
-        d_cp.copy_(d_in)
-    c1.record()
-    torch.cuda.synchronize(dev)
-    copy_gbps = 2 * d_in.numel() * 10 / (c0.elapsed_time(c1) * 1e-3) / 1e9
-    del d_cp
+    # measured on-device copy bandwidth: read + write of this batch's payload buffer, from the
+    # probe before the warm-up steps (or here, with --settle-ms 0)
+    copy_gbps = m["copy_gbps"] or copy_probe(d_in, d_out, 5.0)
+
+    # sustained rate: the same seal launched back to back for --sustain-s seconds on every rank (the clock
+    # under continuous load; outside the timed region above, which stays the reported value)
+    sustained = None
+    if args.sustain_s > 0:
+        n_sus = max(1, int(args.sustain_s * 1e3 / max(kern_ms, 1e-3)))
+        s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        p_recs, p_in, p_aux, p_out, p_tags = (t.data_ptr() for t in (m["d_recs"], d_in, d_aux, d_out, d_tags))
+        eng.join()
+        s0.record(stream)
+        for _ in range(n_sus):
+            eng.seal_batch(p_recs, p_in, p_aux, p_out, p_tags, flags=flags, n=n)
+        eng.join()
+        s1.record(stream)
+        sync()
+        sus_ms = s0.elapsed_time(s1) / n_sus
+        sus_ach = alg_bytes / (sus_ms * 1e-3) / 1e9
+        sustained = {"seconds": round(sus_ms * n_sus / 1e3, 2), "launches": n_sus, "kernel_ms": round(sus_ms, 4),
+                     "GiBps_per_gpu": round(payload / (sus_ms * 1e-3) / 2**30, 3),
+                     "frac": round(sus_ach / HBM_PEAK_GBPS, 4),
+                     "what": "rank 0's seals back to back after the timed steps (HIP events); not the reported value"}
 
     result = None
     if rank == 0:
@@ -514,6 +559,8 @@ def main():
                          "copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(achieved / copy_gbps, 4)},
             "open": m["open"],
         }
+        if sustained:
+            result["sustained"] = sustained
         if world == 1 and not args.no_cpu_baseline:
             sample = min(n, 4096)
             h_in = d_in[: int(recs["in_off"][sample - 1]) + int(recs["len"][sample - 1]) + 16].cpu().numpy()
@@ -602,14 +649,14 @@ def main():
         for name in EXTRA_CONFIGS:
             if name == args.config:
                 continue
-            mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join)
+            mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join, settle_ms=args.settle_ms)
             cfgs[name] = config_summary(name, mm, steps)
             del mm
         if not args.key_slots:
             # SURVEY §8(d)'s worst case: C2 with a key per record (65,536 connections), so no lane groups form
             name = "c2_aes128gcm_64Ki_x_16KiB"
             mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join,
-                         key_slots=workload.CONFIGS[name][1])
+                         key_slots=workload.CONFIGS[name][1], settle_ms=args.settle_ms)
             cfgs[name + " (a key per record)"] = config_summary(name, mm, steps)
             del mm
         if world == 1 and not args.records:
@@ -617,7 +664,7 @@ def main():
             # device-resident launch -- what the 8-GPU config's root holds before it scatters
             name = "c4_aes256gcm_1Mi_x_16KiB"
             mm = measure(name, eng, dev, rank, world, min(steps, 5), min(warmup, 1), not args.no_lazy_join,
-                         records=workload.CONFIGS[name][1])
+                         records=workload.CONFIGS[name][1], settle_ms=args.settle_ms)
             cfgs[name + " (whole batch, 1 GPU)"] = config_summary(name, mm, min(steps, 5))
             del mm
             torch.cuda.empty_cache()

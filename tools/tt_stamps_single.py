@@ -18,7 +18,7 @@ import anothertls_amd as atls  # noqa: E402
 def main():
     fn = atls.library().atls_debug_tt_stamps
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 16)()
     if fn(buf) != 0:
         sys.exit("not a -DATLS_TT_STAMPS build (set ATLS_LIB)")
     out = {"what": "AES-GCM single call: shader-clock cycles per call by phase (gcm_record TT_STAMPS)"}
