@@ -18,7 +18,7 @@ done
 for round in $(seq 1 ${ROUNDS:-3}); do
   for cfg in ${CONFIGS:-c5_mixed_256Ki_x_64B-16KiB}; do
     for lib in $(for v in ${VARIANTS:-base}; do echo anothertls_amd/variants/libatls_$v.so; done); do
-      r=$(ATLS_LIB=$PWD/$lib timeout -k 10 120 python bench.py --config $cfg --no-cpu-baseline --no-configs --steps 20 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'], d['open']['kernel_ms'], d['open']['plaintext_and_status_ok'])") || exit $?
+      r=$(ATLS_LIB=$PWD/$lib timeout -k 10 120 python bench.py --config $cfg --no-cpu-baseline --no-configs --sustain-s 0 --steps 20 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'], d['open']['kernel_ms'], d['open']['plaintext_and_status_ok'])") || exit $?
       echo "round $round $cfg $(basename $lib .so): GiBps seal_ms frac open_ms ok = $r" >> $out
     done
   done

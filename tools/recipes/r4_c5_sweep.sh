@@ -11,7 +11,7 @@ mkdir -p gpurun_out/r4
 cfg=c5_mixed_256Ki_x_64B-16KiB
 run() {  # label, env..., lib
   local label=$1; shift
-  r=$(env "$@" timeout -k 10 120 python bench.py --config $cfg --no-cpu-baseline --no-configs --steps 20 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'], d['open']['kernel_ms'], d['open']['plaintext_and_status_ok'])") || exit 1
+  r=$(env "$@" timeout -k 10 120 python bench.py --config $cfg --no-cpu-baseline --no-configs --sustain-s 0 --steps 20 2>/dev/null | tail -1 | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['roofline']['kernel_ms'], d['roofline']['frac'], d['open']['kernel_ms'], d['open']['plaintext_and_status_ok'])") || exit 1
   echo "round $round $label: GiBps seal_ms frac open_ms ok = $r" >> $out
 }
 ATLS_LIB=$PWD/anothertls_amd/variants/libatls_g8.so timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_plan.py -x -q -m gpu --timeout 200 --timeout-method thread > gpurun_out/r4/c5_sweep_parity_g8.txt 2>&1 || { tail -20 gpurun_out/r4/c5_sweep_parity_g8.txt; exit 1; }
