@@ -328,7 +328,12 @@ __device__ unsigned long long g_tt_stamps[16];
 
 // LAT: the single-call kernel's record (one wave's latency, no occupancy to keep): the branch-free first
 // step (ATLS_SINGLE_FAST_FIRST) and the LDS lane combine at every key size.
-template <int NR, bool OPEN, bool LAT = false>
+// LN: the threads that share the record -- 64 (one wave: the batch kernels), or 256 (the single-call
+// kernel's four waves: slot s goes to thread s mod 256, so a 1.5 KiB record is one step and a 16 KiB one
+// five instead of seventeen). With LN = 256, wb is the base of eight 8 KiB LDS areas: the 4-bit tables of
+// H^64, H^128, H^192 (lane-combine multipliers past H^64) and H^256 (the Horner factor), one per-lane comb
+// area per wave, then 256 B where the waves exchange their partial tags and content-type scans.
+template <int NR, bool OPEN, bool LAT = false, int LN = 64>
 __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx,
                            uint32_t lb, uint32_t wb, int lane) {
   TT_STAMP(t_start);
@@ -411,14 +416,31 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 
   // A record of one step (S <= 64: AEAD up to 976 B in TLS mode) multiplies nothing by H^64:
   // Y starts at 0 and the lane combine applies every power, so it skips the table.
-  const bool one_step = S <= 64u;
-  if (!one_step) {
-    uint32_t seed[4];
+  const bool one_step = S <= (uint32_t)LN;
+  if constexpr (LN == 64) {
+    if (!one_step) {
+      uint32_t seed[4];
 #pragma unroll
-    for (int w = 0; w < 4; w++) seed[w] = k->p4_be[lane >> 1][w];
-    if (!(ATLS_DBG_SKIP & 4)) ghash_table_entries<8>(wb, seed, lane >> 1, (lane & 1) * 8);
-    wave_lds_sync();
+      for (int w = 0; w < 4; w++) seed[w] = k->p4_be[lane >> 1][w];
+      if (!(ATLS_DBG_SKIP & 4)) ghash_table_entries<8>(wb, seed, lane >> 1, (lane & 1) * 8);
+      wave_lds_sync();
+    }
+  } else {
+    // wave b builds the table of H^(64 (b + 1)): H^64 = hpow[63], H^128 = (H^64)^2, H^192 = (H^48)^4,
+    // H^256 = (H^64)^4 -- squarings only; lane l the entries 8 (l & 1) .. +7 of position l / 2
+    if (S > 64u) {
+      const uint32_t b = (uint32_t)lane >> 6, p = ((uint32_t)lane >> 1) & 31u;
+      uint32_t v[4];
+#pragma unroll
+      for (int w = 0; w < 4; w++) v[w] = k->hpow_be[b == 2u ? 47 : 63][w];
+      if (b >= 1u) gf_square(v);
+      if (b >= 2u) gf_square(v);
+      gf_mulxk(v, 4u * p);
+      ghash_table_entries<8>(wb + b * (uint32_t)kGhashBytes, v, (int)p, (lane & 1) * 8);
+    }
+    __syncthreads();
   }
+  const uint32_t wh = LN == 64 ? wb : wb + 3u * (uint32_t)kGhashBytes;  // the Horner factor's table
 
   uint32_t y[4] = {0, 0, 0, 0};
   uint32_t e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // E_K(J0), lane 0
@@ -436,7 +458,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   const uint32_t lane_addr = ((uint32_t)lane << 8) | lb;  // T0 address of byte value `lane`
   const uint32_t k15 = rk[3] >> 24;                       // rk0 byte 15
   CtrCache cc{};
-  if (use_cache) cc = ctr_cache_build(nraw, (uint32_t)lane, rk, rkr, lb);
+  if (use_cache) cc = ctr_cache_build(nraw, (uint32_t)lane & 63u, rk, rkr, lb);
   // AES of this lane's counter block via the cache; j = the step's (wave-uniform) ctr >> 8.
   auto aes_cached = [&](uint32_t (&st4)[4], uint32_t addr1, uint32_t j) {
     const CtrCache cj{(uint32_t)__builtin_amdgcn_readlane((int)cc.u0r, (int)j),
@@ -451,13 +473,22 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   // Lane combine exponent (see below): s_last = the lane's last slot holding a GHASH block (slots
   // 1..m), -1 if none.
   int64_t s_last = -1;
-  if (lane == 0) { if (m >= 64) s_last = (int64_t)(m / 64) * 64; }
-  else if ((uint32_t)lane <= m) s_last = (int64_t)lane + (int64_t)((m - (uint32_t)lane) / 64) * 64;
-  const uint32_t e_comb = s_last >= 1 ? S - (uint32_t)s_last : 1u;  // 1..64
+  if (lane == 0) { if (m >= (uint32_t)LN) s_last = (int64_t)(m / LN) * LN; }
+  else if ((uint32_t)lane <= m) s_last = (int64_t)lane + (int64_t)((m - (uint32_t)lane) / LN) * LN;
+  const uint32_t e_comb = s_last >= 1 ? S - (uint32_t)s_last : 1u;  // 1..LN
   // the lane's combine multiplier H^e_comb, loaded now so its latency hides under the steps
   uint32_t hp[4];
 #pragma unroll
-  for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[e_comb - 1][w];
+  for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[(e_comb - 1u) & 63u][w];
+  if (LN > 64) {  // H^e = H^(e mod 64) * H^(64 kk) by the table of H^(64 kk)
+    const uint32_t kk = (e_comb - 1u) >> 6;
+    if (kk) {
+      uint32_t r[4] = {bswap32(hp[0]), bswap32(hp[1]), bswap32(hp[2]), bswap32(hp[3])};
+      ghash_mul_tab(r, wb + (kk - 1u) * (uint32_t)kGhashBytes);
+#pragma unroll
+      for (int w = 0; w < 4; w++) hp[w] = bswap32(r[w]);
+    }
+  }
 
   // Software pipelining (ATLS_PREFETCH): a fast step issues the load of the next step's block
   // (1 KiB further) before its own AES rounds, so the HBM latency hides under a whole step instead
@@ -465,24 +496,24 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   uint4 Pn = make_uint4(0u, 0u, 0u, 0u);
   bool pref = false, gen_pn = false;
   const uint32_t lim = min(in_bytes, n_aead);
-  const bool first_fast = (LAT ? ATLS_SINGLE_FAST_FIRST : ATLS_GCM_FAST_FIRST) && use_cache && !(OPEN && wire) && fast_end >= 64u;  // TLS / WIRE / RAW (one AAD block)
+  const bool first_fast = (LAT ? ATLS_SINGLE_FAST_FIRST : ATLS_GCM_FAST_FIRST) && use_cache && !(OPEN && wire) && fast_end >= (uint32_t)LN;  // TLS / WIRE / RAW (one AAD block)
   TT_STAMP(t_setup);
-  for (uint32_t base = 0; base < S; base += 64) {
+  for (uint32_t base = 0; base < S; base += LN) {
     TT_STAMP(t_step);
     const uint32_t s = base + (uint32_t)lane;
-    if (base >= 64u && base + 64u <= fast_end) {  // wave-uniform
+    if (base >= (uint32_t)LN && base + LN <= fast_end) {  // wave-uniform
       const uint32_t off = (s - 1u - na) * 16u;
       const uint4 Pu = pref ? Pn : ld16(src + off);
       if (ATLS_PREFETCH) {  // every lane of a fast next step holds a whole block (fast_end)
-        const uint32_t offn = off + 1024u;
-        pref = base + 128u <= fast_end;
+        const uint32_t offn = off + 16u * LN;
+        pref = base + 2u * LN <= fast_end;
         gen_pn = ATLS_GEN_PN && !pref;  // the next step is a general one: its blocks come from Pn too
         Pn = ld16(src + (offn + 16u <= lim ? offn : (ATLS_GEN_PN && offn < lim && lim >= 16u) ? lim - 16u : off));
       }
       const v4u32 P = {Pu.x, Pu.y, Pu.z, Pu.w};
       uint32_t st[4];
       if (use_cache) {
-        const uint32_t c0 = j0[3] + base - na;  // counter of lane 0, a multiple of 64
+        const uint32_t c0 = j0[3] + base - na;  // counter of lane 0, a multiple of LN
         aes_cached(st, lane_addr ^ (((c0 & 0xffu) ^ k15) << 8), c0 >> 8);
       } else {
         st[0] = nraw[0]; st[1] = nraw[1]; st[2] = nraw[2];
@@ -493,7 +524,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       st16(dst + off, make_uint4(C.x, C.y, C.z, C.w));
       if (OPEN && tls) lastnz = block_last_nz(C.x, C.y, C.z, C.w, off, lastnz);
       const v4u32 Bv = OPEN ? P : C;
-      ghash_mul<ATLS_GHASH_W>(y, wb);
+      ghash_mul<ATLS_GHASH_W>(y, wh);
       y[0] ^= Bv.x; y[1] ^= Bv.y; y[2] ^= Bv.z; y[3] ^= Bv.w;
 #ifdef ATLS_TT_STAMPS
       t_fast += __builtin_amdgcn_s_memtime() - t_step;
@@ -508,8 +539,8 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       const uint32_t off = lane >= 2 ? ((uint32_t)lane - 2u) * 16u : 0u;
       const uint4 Pu = ld16(src + off);
       if (ATLS_PREFETCH) {  // the next step's block, as a fast step loads it
-        const uint32_t offn = ((uint32_t)lane + 62u) * 16u;
-        pref = 128u <= fast_end;
+        const uint32_t offn = ((uint32_t)lane + LN - 2u) * 16u;
+        pref = 2u * LN <= fast_end;
         Pn = ld16(src + (offn + 16u <= lim ? offn : off));
       }
       uint32_t st[4];
@@ -602,7 +633,13 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 #endif
     if (use_cache) {  // ctr = 1 for slots 0..na, else 1 + s - na: the step's ctr >> 8 is lane 63's
       const uint32_t ctr = cb[3];
-      const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)ctr, 63) >> 8;
+      uint32_t hi;
+      if constexpr (LN == 64) {
+        hi = (uint32_t)__builtin_amdgcn_readlane((int)ctr, 63) >> 8;
+      } else {  // the step's last slot's counter, across the waves
+        const uint32_t sl = base + LN - 1u;
+        hi = (j0[3] + (sl > na ? sl - na : 0u)) >> 8;
+      }
       aes_cached(st, perm((ctr & 0xffu) ^ k15, lb, 0x0c0c0400u), hi);
     } else {
       aes_encrypt_tt<NR>(st, rk, rkr, lb);
@@ -661,7 +698,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     }
     // Y <- Y * H^64 ^ B on the lanes that hold a GHASH block; the others keep Y (s_last below).
     uint32_t yn[4] = {y[0], y[1], y[2], y[3]};
-    if (base && !(ATLS_DBG_SKIP & 8)) ghash_mul<ATLS_GHASH_W>(yn, wb);  // Y = 0 before the first step
+    if (base && !(ATLS_DBG_SKIP & 8)) ghash_mul<ATLS_GHASH_W>(yn, wh);  // Y = 0 before the first step
     if (s >= 1 && s <= m) {
 #pragma unroll
       for (int w = 0; w < 4; w++) y[w] = yn[w] ^ B[w];
@@ -679,12 +716,40 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
 
   // ---- lane combine: Z = sum_l Y_l * H^(S - s_last(l)) ----
   uint32_t z[4] = {0, 0, 0, 0};
+  const uint32_t wc = LN == 64 ? wb : wb + (4u + ((uint32_t)lane >> 6)) * (uint32_t)kGhashBytes;  // comb area
   if (s_last >= 1) {
     const uint32_t yb[4] = {bswap32(y[0]), bswap32(y[1]), bswap32(y[2]), bswap32(y[3])};
-    lane_comb<NR, LAT>(yb, hp, z, wb, lane);
+    lane_comb<NR, LAT>(yb, hp, z, wc, lane & 63);
   }
 #pragma unroll
   for (int w = 0; w < 4; w++) z[w] = wave_xor(z[w]);
+  const uint32_t xa = wb + 8u * (uint32_t)kGhashBytes;  // LN = 256: the waves' exchange area
+  if (LN > 64) {
+    if (OPEN) {  // the content-type scan's wave maxima travel with the partial tags
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const int64_t o = __shfl_xor(lastnz, off, 64);
+        lastnz = o > lastnz ? o : lastnz;
+      }
+    }
+    if ((lane & 63) == 0) {
+      auto* x4 = reinterpret_cast<__attribute__((address_space(3))) v4u32*>(xa + 16u * ((uint32_t)lane >> 6));
+      *x4 = v4u32{z[0], z[1], z[2], z[3]};
+      if (OPEN) *reinterpret_cast<__attribute__((address_space(3))) int64_t*>(xa + 64u + 8u * ((uint32_t)lane >> 6)) = lastnz;
+    }
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+      for (int w = 1; w < LN / 64; w++) {
+        const v4u32 o = lds_u4(xa + 16u * (uint32_t)w);
+        z[0] ^= o.x; z[1] ^= o.y; z[2] ^= o.z; z[3] ^= o.w;
+        if (OPEN) {
+          const int64_t ol = *reinterpret_cast<const __attribute__((address_space(3))) int64_t*>(xa + 64u + 8u * (uint32_t)w);
+          lastnz = ol > lastnz ? ol : lastnz;
+        }
+      }
+    }
+  }
   const uint32_t t0 = e0 ^ bswap32(z[0]), t1 = e1 ^ bswap32(z[1]), t2 = e2 ^ bswap32(z[2]), t3 = e3 ^ bswap32(z[3]);
 
   if (!OPEN) {
@@ -698,11 +763,13 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       }
     }
   } else {
-    // content-type scan (record.rs:229-237): wave max of (pos << 8 | byte)
+    // content-type scan (record.rs:229-237): wave max of (pos << 8 | byte) (LN = 256: done above)
+    if (LN == 64) {
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const int64_t o = __shfl_xor(lastnz, off, 64);
-      lastnz = o > lastnz ? o : lastnz;
+      for (int off = 32; off >= 1; off >>= 1) {
+        const int64_t o = __shfl_xor(lastnz, off, 64);
+        lastnz = o > lastnz ? o : lastnz;
+      }
     }
     if (lane == 0) {
       const uint4 tg = ld16(wire ? src + len : A.tags_in + 16ull * rec_idx);  // WIRE: tag follows the ct
@@ -1021,7 +1088,7 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
 }
 
 // One record by the whole wave (gcm_record), after the direct-mode descriptor check.
-template <int NR, bool OPEN, bool LAT = false>
+template <int NR, bool OPEN, bool LAT = false, int LN = 64>
 __device__ __forceinline__ void gcm_one(const GcmArgs& A, uint32_t r, uint32_t lb, uint32_t wb, int lane) {
   {
     atls_rec d = A.recs[r];
@@ -1041,7 +1108,7 @@ __device__ __forceinline__ void gcm_one(const GcmArgs& A, uint32_t r, uint32_t l
         return;
       }
     }
-    gcm_record<NR, OPEN, LAT>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
+    gcm_record<NR, OPEN, LAT, LN>(A, d, A.ks + d.key_slot, r, lb, wb, lane);
     wave_lds_sync();  // table reads of this record done before the next record rebuilds it
   }
 }
@@ -1143,6 +1210,29 @@ struct GcmSingle {
   uint8_t bytes[kSingleInline];
 };
 constexpr int kSingleWaves = 4;
+// T-tables, then gcm_record<LN = 256>'s eight 8 KiB areas and its 256-B exchange area
+constexpr size_t kSingleLds = (size_t)kTabBytes + 8u * (size_t)kGhashBytes + 256u;
+static_assert(kSingleLds <= 160u * 1024u, "the single-call kernel's LDS");
+// One record by a 4-wave workgroup (the single call): T-tables, then the record by all four waves
+// (gcm_record LN = 256); every wave's stores have left before wave 0 raises the completion flag.
+template <bool OPEN, int NR>
+__device__ __forceinline__ void single_record(const GcmArgs& A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  smem[kTabBytes / 4 + threadIdx.x] = A.t0[threadIdx.x];  // 256 threads: T0 through the GHASH area
+  __syncthreads();
+  for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
+    const uint32_t v = smem[kTabBytes / 4 + (i >> 6)];
+    smem[i] = (i & 32) ? rotl32(v, 8) : v;
+  }
+  __syncthreads();
+  const int t = (int)threadIdx.x;
+  gcm_one<NR, OPEN, true, 64 * kSingleWaves>(A, 0u, 4u * (uint32_t)(t & 31), (uint32_t)kTabBytes, t);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t < 64) signal_done(A.done, A.done_val, t);
+}
+
 template <bool OPEN, int NR>
 __global__ __launch_bounds__(64 * kSingleWaves) void gcm_single(GcmSingle) {
   // the argument block itself (the only explicit argument, at offset 0), read in place: naming the
@@ -1153,18 +1243,14 @@ __global__ __launch_bounds__(64 * kSingleWaves) void gcm_single(GcmSingle) {
   A.in = S->bytes;
   A.aux = S->bytes;
   if (OPEN) A.tags_in = S->bytes + S->tag_off;
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  smem[kTabBytes / 4 + threadIdx.x] = A.t0[threadIdx.x];  // 256 threads: T0 through the GHASH area
-  __syncthreads();
-  for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
-    const uint32_t v = smem[kTabBytes / 4 + (i >> 6)];
-    smem[i] = (i & 32) ? rotl32(v, 8) : v;
-  }
-  __syncthreads();
-  if (threadIdx.x >= 64) return;
-  const int lane = threadIdx.x & 63;
-  gcm_one<NR, OPEN, true>(A, 0u, 4u * (uint32_t)(lane & 31), (uint32_t)kTabBytes, lane);
-  signal_done(A.done, A.done_val, lane);
+  single_record<OPEN, NR>(A);
+}
+
+// The single call's records that do not fit the argument block: descriptor and data in the pinned block
+// (or a device copy of it), the same 4-wave record.
+template <bool OPEN, int NR>
+__global__ __launch_bounds__(64 * kSingleWaves) void gcm_single_ptr(GcmArgs A) {
+  single_record<OPEN, NR>(A);
 }
 
 }  // namespace atls
@@ -1181,7 +1267,7 @@ extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t
   S.tag_off = tag_off;
   __builtin_memcpy(S.bytes, bytes, nbytes);
   const dim3 block(64 * atls::kSingleWaves);
-  const size_t lds = atls::lds_bytes(1);
+  const size_t lds = atls::kSingleLds;
 #define ATLS_SINGLE(NR)                                                                          \
   if (open) hipLaunchKernelGGL((atls::gcm_single<true, NR>), dim3(1), block, lds, s, S);         \
   else hipLaunchKernelGGL((atls::gcm_single<false, NR>), dim3(1), block, lds, s, S);
@@ -1207,6 +1293,17 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, idx,
                   (atls::PlanHdr*)plan, err, n_slots, idx ? nullptr : gidx,
                   (atls::GroupHdr*)const_cast<uint32_t*>(ghdr), n == 1 ? done : nullptr, done_val};
+  if (n == 1 && done && !idx && !gidx && __builtin_popcount((unsigned)nr_mask) == 1) {  // the single call's longer records: 4 waves
+    const dim3 b1(64 * atls::kSingleWaves);
+#define ATLS_SINGLE_PTR(NR)                                                                            \
+  if (open) hipLaunchKernelGGL((atls::gcm_single_ptr<true, NR>), dim3(1), b1, atls::kSingleLds, s, A);  \
+  else hipLaunchKernelGGL((atls::gcm_single_ptr<false, NR>), dim3(1), b1, atls::kSingleLds, s, A);
+    if (nr_mask & 1) { ATLS_SINGLE_PTR(10) }
+    else if (nr_mask & 2) { ATLS_SINGLE_PTR(12) }
+    else if (nr_mask & 4) { ATLS_SINGLE_PTR(14) }
+#undef ATLS_SINGLE_PTR
+    return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+  }
   static const int waves = [] {
     const char* v = getenv("ATLS_GCM_WAVES");
     const int w = v ? atoi(v) : 12;

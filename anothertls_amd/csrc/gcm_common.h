@@ -234,6 +234,68 @@ __device__ __forceinline__ void gf_mul_comb_lds(const uint32_t (&x)[4], const ui
   z[0] = z0; z[1] = z1; z[2] = z2; z[3] = z3;
 }
 
+// ---- multiplying by x^m and squaring (key setup, the single-call kernel's tables) ----
+// v <- v * x^m in GF(2^128), be words (gf_mulx_be applied m times), 1 <= m <= 64, m may differ per lane.
+// With V the 128-bit number v0:v1:v2:v3 (the coefficient of x^i at bit 127 - i), V * x^m = (V >> m) plus
+// the m low bits pushed past x^127: moved to the top as S = V << (128 - m) they stand for s(x) with
+// V * x^m's overflow = s(x) * x^128 = s(x) * (1 + x + x^2 + x^7) (the 0xE1 of gf_mulx_be), i.e.
+// S ^ S >> 1 ^ S >> 2 ^ S >> 7 -- no second reduction, deg s + 7 < 128.
+__host__ __device__ inline void gf_mulxk64(uint32_t (&v)[4], uint32_t m) {
+  const uint64_t hi = ((uint64_t)v[0] << 32) | v[1], lo = ((uint64_t)v[2] << 32) | v[3];
+  uint64_t rhi, rlo, s;
+  if (m >= 64) {
+    rhi = 0;
+    rlo = hi;
+    s = lo;
+  } else {
+    rhi = hi >> m;
+    rlo = (lo >> m) | (hi << (64 - m));
+    s = lo << (64 - m);
+  }
+  rhi ^= s ^ (s >> 1) ^ (s >> 2) ^ (s >> 7);
+  rlo ^= (s << 63) ^ (s << 62) ^ (s << 57);
+  v[0] = (uint32_t)(rhi >> 32);
+  v[1] = (uint32_t)rhi;
+  v[2] = (uint32_t)(rlo >> 32);
+  v[3] = (uint32_t)rlo;
+}
+
+// v <- v * x^m, 0 <= m <= 127.
+__host__ __device__ inline void gf_mulxk(uint32_t (&v)[4], uint32_t m) {
+  if (m > 64) {
+    gf_mulxk64(v, 64);
+    m -= 64;
+  }
+  if (m) gf_mulxk64(v, m);
+}
+
+// v <- v^2 in GF(2^128), be words. Squaring is linear: the coefficient of x^i moves to x^(2i), i.e. bit
+// b of each 64-bit half to bit 2b+1 of 128 bits; the high half's image stands for O(x) * x^128 =
+// O(x) * (1 + x + x^2 + x^7), folded back with the reducing shifts of gf_mulxk64.
+__device__ __forceinline__ uint64_t spread32(uint32_t x) {  // bit b -> bit 2b
+  uint64_t v = x;
+  v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+  v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+  v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  v = (v | (v << 2)) & 0x3333333333333333ull;
+  v = (v | (v << 1)) & 0x5555555555555555ull;
+  return v;
+}
+__device__ __forceinline__ void gf_square(uint32_t (&v)[4]) {
+  // low half x^0..x^63 (words 0, 1) -> x^0..x^126; high half x^64..x^127 (words 2, 3) -> O(x) * x^128
+  const uint64_t a_hi = spread32(v[0]) << 1, a_lo = spread32(v[1]) << 1;
+  const uint64_t o_hi = spread32(v[2]) << 1, o_lo = spread32(v[3]) << 1;
+  uint32_t o[4] = {(uint32_t)(o_hi >> 32), (uint32_t)o_hi, (uint32_t)(o_lo >> 32), (uint32_t)o_lo};
+  uint32_t o1[4] = {o[0], o[1], o[2], o[3]}, o2[4] = {o[0], o[1], o[2], o[3]}, o7[4] = {o[0], o[1], o[2], o[3]};
+  gf_mulxk64(o1, 1);
+  gf_mulxk64(o2, 2);
+  gf_mulxk64(o7, 7);
+  v[0] = (uint32_t)(a_hi >> 32) ^ o[0] ^ o1[0] ^ o2[0] ^ o7[0];
+  v[1] = (uint32_t)a_hi ^ o[1] ^ o1[1] ^ o2[1] ^ o7[1];
+  v[2] = (uint32_t)(a_lo >> 32) ^ o[2] ^ o1[2] ^ o2[2] ^ o7[2];
+  v[3] = (uint32_t)a_lo ^ o[3] ^ o1[3] ^ o2[3] ^ o7[3];
+}
+
 // XOR of x over the wave without the LDS (ds_bpermute) path of __shfl_xor: four DPP steps leave
 // every lane with its 16-lane row's XOR (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
 // row_mirror), then four v_readlane combine the rows. Wave-uniform result.

@@ -15,7 +15,7 @@
 //     power 2^k lanes below by H^(2^k), one factor for the whole wave -- each product by a 4-bit table of
 //     that factor built in the wave's LDS (gcm_common.h ghash_table_entries / ghash_mul_tab, the record
 //     kernels' own GHASH machinery: 32 lookups per product instead of a 128-step bit-serial loop);
-//   * every table seed x^k * Y is one shift and one reduction (gf_mulxk below), so the 32 seeds of a table
+//   * every table seed x^k * Y is one shift and one reduction (gcm_common.h gf_mulxk), so the 32 seeds of a table
 //     and the 128 record-table seeds are computed by all lanes at once.
 #include "aes_sbox.h"
 #include "gcm_common.h"
@@ -29,40 +29,6 @@ __device__ __forceinline__ uint32_t t0_entry(int x) {
 }
 
 __global__ void build_t0_kernel(uint32_t* __restrict__ t0) { t0[threadIdx.x] = t0_entry((int)threadIdx.x); }
-
-// v <- v * x^m in GF(2^128), be words (gf_mulx_be applied m times), 1 <= m <= 64, m may differ per lane.
-// With V the 128-bit number v0:v1:v2:v3 (the coefficient of x^i at bit 127 - i), V * x^m = (V >> m) plus
-// the m low bits pushed past x^127: moved to the top as S = V << (128 - m) they stand for s(x) with
-// V * x^m's overflow = s(x) * x^128 = s(x) * (1 + x + x^2 + x^7) (the 0xE1 of gf_mulx_be), i.e.
-// S ^ S >> 1 ^ S >> 2 ^ S >> 7 -- no second reduction, deg s + 7 < 128.
-__host__ __device__ inline void gf_mulxk64(uint32_t (&v)[4], uint32_t m) {
-  const uint64_t hi = ((uint64_t)v[0] << 32) | v[1], lo = ((uint64_t)v[2] << 32) | v[3];
-  uint64_t rhi, rlo, s;
-  if (m >= 64) {
-    rhi = 0;
-    rlo = hi;
-    s = lo;
-  } else {
-    rhi = hi >> m;
-    rlo = (lo >> m) | (hi << (64 - m));
-    s = lo << (64 - m);
-  }
-  rhi ^= s ^ (s >> 1) ^ (s >> 2) ^ (s >> 7);
-  rlo ^= (s << 63) ^ (s << 62) ^ (s << 57);
-  v[0] = (uint32_t)(rhi >> 32);
-  v[1] = (uint32_t)rhi;
-  v[2] = (uint32_t)(rlo >> 32);
-  v[3] = (uint32_t)rlo;
-}
-
-// v <- v * x^m, 0 <= m <= 127.
-__host__ __device__ inline void gf_mulxk(uint32_t (&v)[4], uint32_t m) {
-  if (m > 64) {
-    gf_mulxk64(v, 64);
-    m -= 64;
-  }
-  if (m) gf_mulxk64(v, m);
-}
 
 // The wave's 4-bit table of the wave-uniform factor y (be words) at LDS byte address wb: lane l writes
 // entries 8 (l & 1) .. +7 of position l >> 1 from the seed x^(4p) * y (gcm_common.h layout).
@@ -142,33 +108,6 @@ struct KeySetupArgs {
   uint32_t inl[kInlineKeys][16];
 };
 static_assert(sizeof(atls_key) == 64, "atls_key is 16 words");
-
-// v <- v^2 in GF(2^128), be words. Squaring is linear: the coefficient of x^i moves to x^(2i), i.e. bit
-// b of each 64-bit half to bit 2b+1 of 128 bits; the high half's image stands for O(x) * x^128 =
-// O(x) * (1 + x + x^2 + x^7), folded back with the reducing shifts of gf_mulxk64.
-__device__ __forceinline__ uint64_t spread32(uint32_t x) {  // bit b -> bit 2b
-  uint64_t v = x;
-  v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
-  v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
-  v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
-  v = (v | (v << 2)) & 0x3333333333333333ull;
-  v = (v | (v << 1)) & 0x5555555555555555ull;
-  return v;
-}
-__device__ __forceinline__ void gf_square(uint32_t (&v)[4]) {
-  // low half x^0..x^63 (words 0, 1) -> x^0..x^126; high half x^64..x^127 (words 2, 3) -> O(x) * x^128
-  const uint64_t a_hi = spread32(v[0]) << 1, a_lo = spread32(v[1]) << 1;
-  const uint64_t o_hi = spread32(v[2]) << 1, o_lo = spread32(v[3]) << 1;
-  uint32_t o[4] = {(uint32_t)(o_hi >> 32), (uint32_t)o_hi, (uint32_t)(o_lo >> 32), (uint32_t)o_lo};
-  uint32_t o1[4] = {o[0], o[1], o[2], o[3]}, o2[4] = {o[0], o[1], o[2], o[3]}, o7[4] = {o[0], o[1], o[2], o[3]};
-  gf_mulxk64(o1, 1);
-  gf_mulxk64(o2, 2);
-  gf_mulxk64(o7, 7);
-  v[0] = (uint32_t)(a_hi >> 32) ^ o[0] ^ o1[0] ^ o2[0] ^ o7[0];
-  v[1] = (uint32_t)a_hi ^ o[1] ^ o1[1] ^ o2[1] ^ o7[1];
-  v[2] = (uint32_t)(a_lo >> 32) ^ o[2] ^ o1[2] ^ o2[2] ^ o7[2];
-  v[3] = (uint32_t)a_lo ^ o[3] ^ o1[3] ^ o2[3] ^ o7[3];
-}
 
 // Phase clocks of a key install (timing build -DATLS_KS_STAMPS, tools/key_setup_stamps.py): lane 0 of wave
 // 0 of key 0 adds the shader clock at each phase end (after its memory operations) to g_ks_stamps[i];

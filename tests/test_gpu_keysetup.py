@@ -38,7 +38,7 @@ def test_model_product_equals_oracle_gmult():
 
 
 def _mulxk64(v, m):
-    """keysetup.hip gf_mulxk64, restated on a Python int (1 <= m <= 64): shift, and the m bits pushed
+    """gcm_common.h gf_mulxk64, restated on a Python int (1 <= m <= 64): shift, and the m bits pushed
     past x^127 folded back as S ^ S>>1 ^ S>>2 ^ S>>7."""
     mask = (1 << 128) - 1
     s = (v << (128 - m)) & mask
@@ -126,7 +126,7 @@ def test_many_keys_one_launch_match_model():
 
 
 def _square(v):
-    """keysetup.hip gf_square, restated on a Python int: coefficient x^i -> x^(2i) (bit b of each 64-bit
+    """gcm_common.h gf_square, restated on a Python int: coefficient x^i -> x^(2i) (bit b of each 64-bit
     half -> bit 2b + 1), the high half's image O(x) folded back as O * (1 + x + x^2 + x^7)."""
     def spread(x):
         return sum(((x >> b) & 1) << (2 * b + 1) for b in range(64))
