@@ -240,7 +240,17 @@ typedef uint32_t v4u32_ch __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4u32_ch lds_uint4;
 // PRE: 0 = a slot's data is loaded where it is used (after its keystream); 1 = at the top of its step,
 // before the keystream; 2 = one step ahead, before the previous step's stores (chacha_kernel_w2).
-template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G == 64 ? 1 : 0, bool STAGE = false>
+// The single call's records beyond the argument block (> 3.5 KiB: more than one 64-lane step from ~4 KiB)
+// take 4 waves (G = 256: 16,385 B seal 32.5 -> 23.2 us); those in the argument block stay on one wave,
+// where the 4-wave record measured slower (1,537 B seal 15.4 -> 17.1 us: barriers, exchange, a fuller scan).
+#ifndef ATLS_CHACHA_SINGLE_4W
+#define ATLS_CHACHA_SINGLE_4W 1
+#endif
+constexpr int kChSingleThreads = 64;
+// G = 256: one record on a 4-wave workgroup (the single call; slot j on thread j mod 256): lane scans and
+// reductions run per wave, the waves meet in LDS (Poly1305 key broadcast, partial tags, content-type scan),
+// and wave w's powers carry the factor r^(256 w) (r^256 = its lane 63's (r^4)^64).
+template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G >= 64 ? 1 : 0, bool STAGE = false>
 __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched* k, uint32_t rec_idx, int gl,
                               lds_uint4* lds = nullptr) {
   // TLS and WIRE: nonce from (static IV, seq), 5-byte AAD; WIRE also frames the record
@@ -288,6 +298,8 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   // r powers: r, rsq = r^2, rcu = r^3 in every lane; R = (r^4)^(gl+1) by a prefix-product scan over the 16
   // lanes of the group (4 levels); r64 = r^64 (lane 15's R).
   P130 r = p_zero(), rsq = p_zero(), rcu = p_zero(), R = p_zero(), r64 = p_zero();
+  constexpr int GW = G > 64 ? 64 : G;  // lanes of one wave in the group
+  P130 r256 = p_zero(), r512 = p_zero(), r768 = p_zero();  // G = 256: wave factors
   uint32_t sk[4] = {0, 0, 0, 0};
   P130 acc = p_zero(), innerL = p_zero();
   int64_t lastnz = -1;
@@ -386,8 +398,20 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     if (G == 64 && base == 0) LAT_STAMP(3, gl == 0);  // keystream blocks
     if (base == 0) {
       // Poly1305 one-time key from block 0 (poly1305.rs:19-22), broadcast within the group.
-      uint32_t r0 = __shfl(ks[0], 0, G), r1 = __shfl(ks[1], 0, G), r2 = __shfl(ks[2], 0, G), r3 = __shfl(ks[3], 0, G);
-      sk[0] = __shfl(ks[4], 0, G); sk[1] = __shfl(ks[5], 0, G); sk[2] = __shfl(ks[6], 0, G); sk[3] = __shfl(ks[7], 0, G);
+      uint32_t r0, r1, r2, r3;
+      if constexpr (G > 64) {
+        __shared__ uint32_t bc[8];
+        if (gl == 0) {
+#pragma unroll
+          for (int i = 0; i < 8; i++) bc[i] = ks[i];
+        }
+        __syncthreads();
+        r0 = bc[0]; r1 = bc[1]; r2 = bc[2]; r3 = bc[3];
+        sk[0] = bc[4]; sk[1] = bc[5]; sk[2] = bc[6]; sk[3] = bc[7];
+      } else {
+        r0 = __shfl(ks[0], 0, G); r1 = __shfl(ks[1], 0, G); r2 = __shfl(ks[2], 0, G); r3 = __shfl(ks[3], 0, G);
+        sk[0] = __shfl(ks[4], 0, G); sk[1] = __shfl(ks[5], 0, G); sk[2] = __shfl(ks[6], 0, G); sk[3] = __shfl(ks[7], 0, G);
+      }
       r0 &= 0x0fffffffu; r1 &= 0x0ffffffcu; r2 &= 0x0ffffffcu; r3 &= 0x0ffffffcu;  // clamp (:26)
       r.l[0] = r0 & M26;
       r.l[1] = ((r0 >> 26) | (r1 << 6)) & M26;
@@ -398,17 +422,24 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       R = p_mul(rsq, rsq);  // r^4
       if (!LATE) rcu = p_mul(rsq, r);
 #pragma unroll
-      for (int d = 1; d < G; d <<= 1) {  // Hillis-Steele prefix product
+      for (int d = 1; d < GW; d <<= 1) {  // Hillis-Steele prefix product (G = 256: within each wave)
         // one record per wave (the single call): lanes past jL hold no slot, so a record of one step
         // (jL < 32: up to ~1.9 KiB) stops after the levels lanes 0..jL need (5 for an MTU-sized record)
         if (G == 64 && (uint32_t)d > jL) continue;
         P130 t;
 #pragma unroll
-        for (int i = 0; i < 5; i++) t.l[i] = __shfl_up(R.l[i], (unsigned)d, G);
+        for (int i = 0; i < 5; i++) t.l[i] = __shfl_up(R.l[i], (unsigned)d, GW);
         const P130 m = p_mul(R, t);
-        if (gl >= d) R = m;
+        if ((gl & (GW - 1)) >= d) R = m;
       }
-      r64 = shfl_p<G>(R, G - 1);
+      if constexpr (G > 64) {  // (r^4)^(l+1) per wave lane l; r^(4G) = r^1024 for the slot Horner
+        r256 = shfl_p<64>(R, 63);
+        r512 = p_mul(r256, r256);
+        r768 = p_mul(r512, r256);
+        r64 = p_mul(r512, r512);
+      } else {
+        r64 = shfl_p<G>(R, G - 1);
+      }
       if (G == 64) LAT_STAMP(4, gl == 0);  // r powers (lane scan)
     }
     if (!active) continue;
@@ -594,10 +625,18 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     if (jL >= 1 && l <= jL - 1) {
       const uint32_t jf = l + ((jL - 1 - l) / G) * G;
       const uint32_t ref = (jf == 0) ? na - 1u : na + 4u * jf - 1u;
-      const uint32_t e = Q - ref;  // 1..65
-      // r^e = r^(e mod 4) * (r^4)^(e >> 2); (r^4)^u is lane u-1's R
+      const uint32_t e = Q - ref;  // 1..4G+1
+      // r^e = r^(e mod 4) * (r^4)^(e >> 2); (r^4)^u is lane u-1's R (G = 256: lane (u-1) mod 64's R of
+      // any wave times r^(256 ((u-1) >> 6)))
       const uint32_t u = e >> 2, c = e & 3u;
-      P130 ru = shfl_p<G>(R, (int)(u ? u - 1u : 0u));
+      P130 ru;
+      if constexpr (G > 64) {
+        const uint32_t ix = u ? u - 1u : 0u, wq = ix >> 6;
+        ru = shfl_p<64>(R, (int)(ix & 63u));
+        if (wq) ru = p_mul(ru, wq == 1u ? r256 : wq == 2u ? r512 : r768);
+      } else {
+        ru = shfl_p<G>(R, (int)(u ? u - 1u : 0u));
+      }
       if (u == 0) { ru = p_zero(); ru.l[0] = 1; }
       P130 pw;
       if (c == 0) pw = ru;
@@ -612,10 +651,35 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     }
     if (l == jL % G) p_add(contrib, p_mul(innerL, r));
   }
-  for (int off = G / 2; off >= 1; off >>= 1) {
+  for (int off = GW / 2; off >= 1; off >>= 1) {
     P130 o = p_zero();
-    for (int i = 0; i < 5; i++) o.l[i] = __shfl_xor(contrib.l[i], off, G);
+    for (int i = 0; i < 5; i++) o.l[i] = __shfl_xor(contrib.l[i], off, GW);
     p_add(contrib, o);
+  }
+  if constexpr (G > 64) {  // the waves' partial sums (and content-type maxima) meet in LDS
+    if (OPEN) {
+      for (int off = 32; off >= 1; off >>= 1) {
+        const int64_t o = __shfl_xor(lastnz, off, 64);
+        lastnz = o > lastnz ? o : lastnz;
+      }
+    }
+    __shared__ uint32_t xc[G / 64][5];
+    __shared__ int64_t xl[G / 64];
+    p_carry(contrib);  // limbs < 2^26 again, so four partials add without overflow
+    if ((gl & 63) == 0) {
+#pragma unroll
+      for (int i = 0; i < 5; i++) xc[gl >> 6][i] = contrib.l[i];
+      xl[gl >> 6] = lastnz;
+    }
+    __syncthreads();
+    if (gl == 0) {
+#pragma unroll
+      for (int w = 1; w < G / 64; w++) {
+#pragma unroll
+        for (int i = 0; i < 5; i++) contrib.l[i] += xc[w][i];
+        lastnz = xl[w] > lastnz ? xl[w] : lastnz;
+      }
+    }
   }
   uint32_t tag[4];
   p_finish(contrib, sk, tag);
@@ -633,9 +697,11 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       }
     }
   } else {
-    for (int off = G / 2; off >= 1; off >>= 1) {
-      const int64_t o = __shfl_xor(lastnz, off, G);
-      lastnz = o > lastnz ? o : lastnz;
+    if (G <= 64) {
+      for (int off = G / 2; off >= 1; off >>= 1) {
+        const int64_t o = __shfl_xor(lastnz, off, G);
+        lastnz = o > lastnz ? o : lastnz;
+      }
     }
     if (gl == 0) {
       const uint4 tg = ld16(wire ? src + len : A.tags_in + 16ull * rec_idx);  // WIRE: tag follows the ct
@@ -894,7 +960,7 @@ struct ChSingle {
   uint8_t bytes[kSingleInline];
 };
 template <bool OPEN>
-__global__ __launch_bounds__(64) void chacha_single(ChSingle) {
+__global__ __launch_bounds__(kChSingleThreads) void chacha_single(ChSingle) {
   // the argument block itself (the only explicit argument, at offset 0), read in place: naming the
   // by-value parameter's members by address would copy all of it to scratch first
   const ChSingle* S = (const ChSingle*)__builtin_amdgcn_kernarg_segment_ptr();
@@ -911,14 +977,27 @@ __global__ __launch_bounds__(64) void chacha_single(ChSingle) {
   }
   LAT_STAMP(0, threadIdx.x == 0);
 #endif
-  chacha_group<OPEN, 64, false>(A, W, 0u, 1u, (int)(threadIdx.x & 63));
+  chacha_group<OPEN, kChSingleThreads, false>(A, W, 0u, 1u, (int)threadIdx.x);  // one record on all the waves
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's stores have left
 #ifdef ATLS_LAT_STAMPS
   LAT_STAMP(7, threadIdx.x == 0);  // outputs written to the caller's mapped memory
   if (threadIdx.x == 0) atomicAdd(&g_lat_stamps[9], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
-  if ((threadIdx.x & 63) == 0) __hip_atomic_store(A.done, A.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) __hip_atomic_store(A.done, A.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The single call's records that do not fit the argument block (descriptor and data in the pinned block),
+// on the same 4-wave record.
+template <bool OPEN>
+__global__ __launch_bounds__(256) void chacha_single_ptr(ChArgs A) {
+  const WorkList W{nullptr, nullptr, kListChacha, 1u};
+  chacha_group<OPEN, 256, false>(A, W, 0u, 1u, (int)threadIdx.x);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(A.done, A.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace atls
@@ -959,8 +1038,8 @@ extern "C" int atls_launch_chacha_single(int open, const void* ks, uint32_t n_sl
   S.d = *d;
   S.tag_off = tag_off;
   __builtin_memcpy(S.bytes, bytes, nbytes);
-  if (open) hipLaunchKernelGGL((atls::chacha_single<true>), dim3(1), dim3(64), 0, s, S);
-  else hipLaunchKernelGGL((atls::chacha_single<false>), dim3(1), dim3(64), 0, s, S);
+  if (open) hipLaunchKernelGGL((atls::chacha_single<true>), dim3(1), dim3(atls::kChSingleThreads), 0, s, S);
+  else hipLaunchKernelGGL((atls::chacha_single<false>), dim3(1), dim3(atls::kChSingleThreads), 0, s, S);
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
 
@@ -977,7 +1056,10 @@ extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs
   // strides over 16 positions per wave and simply finishes its list sooner
   const uint32_t want16 = (n + 15u) / 16u;
   const uint32_t g = (uint32_t)grid < want16 ? (uint32_t)grid : want16;
-  if (!idx && n <= (uint32_t)ATLS_CHACHA_LAT_MAX) {
+  if (ATLS_CHACHA_SINGLE_4W && !idx && n == 1 && done) {  // the single call's longer records: 4 waves
+    if (open) hipLaunchKernelGGL((atls::chacha_single_ptr<true>), dim3(1), dim3(256), 0, s, A);
+    else hipLaunchKernelGGL((atls::chacha_single_ptr<false>), dim3(1), dim3(256), 0, s, A);
+  } else if (!idx && n <= (uint32_t)ATLS_CHACHA_LAT_MAX) {
     if (open) hipLaunchKernelGGL((atls::chacha_kernel_lat<true>), dim3(n), dim3(64), 0, s, A);
     else hipLaunchKernelGGL((atls::chacha_kernel_lat<false>), dim3(n), dim3(64), 0, s, A);
   } else if (idx) {

@@ -162,3 +162,48 @@ def test_single_first_step_boundary_vs_oracle(suite, klen):
             assert c.decrypt(key, iv, ct, aad, tag) == pt
             with pytest.raises(atls.TlsError):
                 c.decrypt(key, iv, ct, aad, bytes([tag[0] ^ 1]) + tag[1:])
+
+
+@pytest.mark.parametrize("suite,klen", [(0x1301, 16), (0x1302, 32)])
+def test_four_wave_step_boundaries_vs_oracle(suite, klen):
+    """The AES-GCM single call spreads a record over four waves (gcm.hip gcm_record LN = 256: 256 slots per
+    step, H^256 Horner, combine multipliers up to H^256): records whose slot count lands on each side of
+    256 / 512 / 1,024, in the argument block and from the pinned block, 12- and 16-byte IVs, AADs of 0-40
+    bytes; seal, open and a tampered tag against the oracle."""
+    rng = random.Random(klen * 31 + suite)
+    key = bytes(rng.getrandbits(8) for _ in range(klen))
+    c = atls.CipherSuite(suite).get_cipher()
+    for iv_len in (12, 16):
+        for aad_len in (0, 5, 40):
+            for n in (976, 992, 1008, 3520, 4064, 4080, 4096, 8160, 8176, 8192, 16336, 16352, 16368, 16385):
+                iv = bytes(rng.getrandbits(8) for _ in range(iv_len))
+                aad = bytes(rng.getrandbits(8) for _ in range(aad_len))
+                pt = bytes(rng.getrandbits(8) for _ in range(n))
+                ct, tag = c.encrypt(key, iv, pt, aad)
+                rc, ect, etag = ora.cipher_encrypt(suite, key, iv, pt, aad)
+                assert rc == 0 and ct == ect and tag == etag, (iv_len, aad_len, n)
+                assert c.decrypt(key, iv, ct, aad, tag) == pt
+                with pytest.raises(atls.TlsError):
+                    c.decrypt(key, iv, ct, aad, tag[:8] + bytes([tag[8] ^ 4]) + tag[9:])
+
+
+def test_chacha_four_wave_record_vs_oracle():
+    """The ChaCha20-Poly1305 single call on four waves (chacha.hip chacha_record G = 256: slot j on thread
+    j mod 256, per-wave power scans with the wave factor r^(256 w), the Horner factor r^1024, partial tags
+    and content-type maxima meeting in LDS): lengths from empty to past one 256-slot step (16,305 B and
+    up take two), the F4 quirk lengths (n % 64 == 0, cipher.rs:99-102), AADs of 0-40 bytes; seal, open
+    and a tampered tag against the oracle."""
+    rng = random.Random(0xC4A)
+    key = bytes(rng.getrandbits(8) for _ in range(32))
+    c = atls.CipherSuite(0x1303).get_cipher()
+    for aad_len in (0, 5, 40):
+        for n in (0, 1, 63, 64, 65, 1536, 1537, 3500, 4096, 8191, 16304, 16320, 16336, 16383, 16384, 16385):
+            iv = bytes(rng.getrandbits(8) for _ in range(12))
+            aad = bytes(rng.getrandbits(8) for _ in range(aad_len))
+            pt = bytes(rng.getrandbits(8) for _ in range(n))
+            ct, tag = c.encrypt(key, iv, pt, aad)
+            rc, ect, etag = ora.cipher_encrypt(0x1303, key, iv, pt, aad)
+            assert rc == 0 and ct == ect and tag == etag, (aad_len, n)
+            assert c.decrypt(key, iv, ct, aad, tag) == pt
+            with pytest.raises(atls.TlsError):
+                c.decrypt(key, iv, ct, aad, tag[:15] + bytes([tag[15] ^ 0x40]))

@@ -2,7 +2,9 @@
 at a -DATLS_LAT_STAMPS build (anothertls_amd/variants/libatls_latstamps.so, tools/recipes/r4_single.sh).
 The kernel's lane 0 adds the shader clock at each phase end to a device array (after waiting for its
 outstanding memory operations); the real-time clock at entry / exit calibrates cycles to microseconds.
-Prints one JSON object: the host-side median per call and the mean kernel phases. Needs a GPU."""
+Prints one JSON object: the host-side median per call and the mean kernel phases. Needs a GPU.
+The phase stamps sit in the one-wave record (chacha_record G = 64), which the single call used until the
+4-wave record replaced it later in round 4 (G = 256); profiles/r04/single_call_stamps.json is from then."""
 import ctypes
 import json
 import os
