@@ -428,8 +428,10 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   } else {
     // wave b builds the table of H^(64 (b + 1)): H^64 = hpow[63], H^128 = (H^64)^2, H^192 = (H^48)^4,
     // H^256 = (H^64)^4 -- squarings only; lane l the entries 8 (l & 1) .. +7 of position l / 2
-    if (S > 64u) {
-      const uint32_t b = (uint32_t)lane >> 6, p = ((uint32_t)lane >> 1) & 31u;
+    // (only the tables this record uses: H^(64 (b+1)) when some lane's e - 1 reaches it, H^256 past one step)
+    const uint32_t b = (uint32_t)lane >> 6;
+    if (b < 3u ? S >= 64u * (b + 1u) + 2u : S > (uint32_t)LN) {
+      const uint32_t p = ((uint32_t)lane >> 1) & 31u;
       uint32_t v[4];
 #pragma unroll
       for (int w = 0; w < 4; w++) v[w] = k->hpow_be[b == 2u ? 47 : 63][w];
