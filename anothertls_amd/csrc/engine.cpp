@@ -40,6 +40,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
                                const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
 extern "C" size_t atls_group_hdr_offset(uint32_t n_slots);
+extern "C" int atls_launch_sync_flag(const uint32_t* err, uint32_t* out, uint32_t val, hipStream_t s);
 extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t n_slots, const atls_rec* d,
                                       const uint8_t* bytes, uint32_t nbytes, uint32_t tag_off, uint8_t* out,
                                       uint8_t* tags_out, atls_open_result* res, const uint32_t* t0, uint32_t* err,
@@ -86,6 +87,9 @@ struct DevBuf {
 
 }  // namespace
 
+#ifndef ATLS_SYNC_FLAG_DEFAULT
+#define ATLS_SYNC_FLAG_DEFAULT 0  // 1: synchronous returns wait on the sync-flag kernel (finish); env ATLS_SYNC_FLAG overrides
+#endif
 struct atls_engine {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -120,6 +124,12 @@ struct atls_engine {
   hipStream_t up = nullptr, down = nullptr;
   std::vector<hipEvent_t> pev;
   int zero_copy = 0;  // ATLS_ZERO_COPY: 1 = kernels read and write pinned host buffers in place, 2 = write only
+  // Synchronous returns (finish): a mapped word pair the sync-flag kernel writes -- [0] completion value,
+  // [1] the sticky error word -- instead of hipStreamSynchronize + a copy (ATLS_SYNC_FLAG=0: the old way)
+  uint32_t* sync_h = nullptr;
+  uint32_t* sync_d = nullptr;
+  uint32_t sync_val = 0;
+  int sync_flag = ATLS_SYNC_FLAG_DEFAULT;
   std::mutex mu;
 };
 
@@ -147,12 +157,56 @@ int join_pending(atls_engine* e) {
   return ATLS_OK;
 }
 
-int finish(atls_engine* e, uint32_t flags) {
+// The sync-flag block (mapped, page-locked), allocated on first use; false: use the stream sync.
+bool sync_flag_ready(atls_engine* e) {
+  if (!e->sync_flag) return false;
+  if (e->sync_h) return true;
+  void* p = nullptr;
+  void* pd = nullptr;
+  if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    e->sync_flag = 0;
+    return false;
+  }
+  if (hipHostGetDevicePointer(&pd, p, 0) != hipSuccess) {
+    (void)hipHostFree(p);
+    e->sync_flag = 0;
+    return false;
+  }
+  std::memset(p, 0, 64);
+  e->sync_h = (uint32_t*)p;
+  e->sync_d = (uint32_t*)pd;
+  return true;
+}
+
+// host_copies: the stream holds copies into the caller's host memory, which may be pageable -- the runtime
+// finishes those on the host after the device is done with them, so only a stream synchronisation covers them.
+int finish(atls_engine* e, uint32_t flags, bool host_copies = false) {
   if (flags & ATLS_FLAG_NO_SYNC) return ATLS_OK;
   if (join_pending(e)) return ATLS_INTERNAL_ERROR;
-  if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
   uint32_t err = 0;
-  if (hipMemcpy(&err, e->err.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  if (!host_copies && sync_flag_ready(e)) {
+    // everything before it on the engine stream has finished once the flag reads v; a stream that ends
+    // without it (a fault) is reported by hipStreamQuery, checked every few thousand spins
+    const uint32_t v = ++e->sync_val;
+    __atomic_store_n(&e->sync_h[0], v - 1u, __ATOMIC_RELEASE);
+    if (atls_launch_sync_flag((const uint32_t*)e->err.p, e->sync_d, v, e->stream)) return ATLS_INTERNAL_ERROR;
+    for (uint64_t i = 1;; i++) {
+      if (__atomic_load_n(&e->sync_h[0], __ATOMIC_ACQUIRE) == v) break;
+      if ((i & 4095) == 0) {
+        const hipError_t q = hipStreamQuery(e->stream);
+        if (q == hipSuccess) {
+          if (__atomic_load_n(&e->sync_h[0], __ATOMIC_ACQUIRE) == v) break;
+          return ATLS_INTERNAL_ERROR;
+        }
+        if (q != hipErrorNotReady) return ATLS_INTERNAL_ERROR;
+      }
+      __builtin_ia32_pause();
+    }
+    err = __atomic_load_n(&e->sync_h[1], __ATOMIC_ACQUIRE);
+  } else {
+    if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
+    if (hipMemcpy(&err, e->err.p, 4, hipMemcpyDeviceToHost) != hipSuccess) return ATLS_INTERNAL_ERROR;
+  }
   return take_err(e, err);
 }
 
@@ -341,7 +395,7 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   // the engine stream is ordered after the last download (finish synchronises it)
   if (!zo && (hipEventRecord(e->ev_side, down) != hipSuccess || hipStreamWaitEvent(ks, e->ev_side, 0) != hipSuccess))
     return fail(ATLS_INTERNAL_ERROR);
-  return finish(e, 0);
+  return finish(e, 0, true);
 }
 
 int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
@@ -522,7 +576,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     if (open && hipMemcpyAsync(res, e->res.p, sizeof(atls_open_result) * (size_t)n, hipMemcpyDeviceToHost, s) !=
                     hipSuccess)
       return ATLS_INTERNAL_ERROR;
-    return finish(e, flags & ~ATLS_FLAG_NO_SYNC);
+    return finish(e, flags & ~ATLS_FLAG_NO_SYNC, true);
   }
   return finish(e, flags);
 }
@@ -930,6 +984,7 @@ atls_engine* atls_engine_create(int device) {
   if (const char* v = std::getenv("ATLS_CHACHA_W2")) e->chacha_w2 = std::atoi(v);
   if (const char* v = std::getenv("ATLS_ZERO_COPY")) e->zero_copy = std::atoi(v);
   if (const char* v = std::getenv("ATLS_GCM_GROUP_MIN")) e->group_min = (uint32_t)std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("ATLS_SYNC_FLAG")) e->sync_flag = std::atoi(v) != 0;
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || hipMemsetAsync(e->err.p, 0, 16, e->stream) != hipSuccess ||
       atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
       hipStreamSynchronize(e->stream) != hipSuccess) {
@@ -958,6 +1013,7 @@ void atls_engine_destroy(atls_engine* e) {
   if (e->down) (void)hipStreamDestroy(e->down);
   if (e->stream2) (void)hipStreamDestroy(e->stream2);
   if (e->stream) (void)hipStreamDestroy(e->stream);
+  if (e->sync_h) (void)hipHostFree(e->sync_h);
   delete e;
 }
 
@@ -1111,7 +1167,7 @@ int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* 
     return ATLS_INTERNAL_ERROR;
   if (!dev) {
     if (hipMemcpyAsync(out, e->out.p, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
-    return finish(e, flags & ~ATLS_FLAG_NO_SYNC);
+    return finish(e, flags & ~ATLS_FLAG_NO_SYNC, true);
   }
   return finish(e, flags);
 }

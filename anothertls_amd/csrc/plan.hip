@@ -254,7 +254,25 @@ __global__ __launch_bounds__(256) void group_place(const atls_rec* recs, uint32_
   }
 }
 
+
+// The engine's synchronous return (engine.cpp finish): after everything before it on the engine stream,
+// one lane copies the sticky error word and then a completion value into mapped host memory, with a
+// system-scope release between them, so the host spins on a flag (~6 us on this box) instead of
+// hipStreamSynchronize plus a device-to-host copy of the error word (~11 us + a copy).
+__global__ void sync_flag_kernel(const uint32_t* err, uint32_t* out, uint32_t val) {
+  if (threadIdx.x == 0) {
+    out[1] = *reinterpret_cast<const volatile uint32_t*>(err);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store(out, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace atls
+
+extern "C" int atls_launch_sync_flag(const uint32_t* err, uint32_t* out, uint32_t val, hipStream_t s) {
+  hipLaunchKernelGGL(atls::sync_flag_kernel, dim3(1), dim3(64), 0, s, err, out, val);
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}
 
 // Key groups of a direct batch. cnt: 2 * (n_slots + 1) words (counts, cursors), zero on entry and
 // on return. aux: 3 arrays of n_slots + 1 words followed by the GroupHdr (atls_group_hdr_offset

@@ -1,7 +1,8 @@
 // Latency floor of one Cipher-trait call on this box, through the C ABI (no Python): the median
 // microseconds of (a) an empty kernel launch + hipStreamSynchronize, (b) an empty kernel launch
 // whose one lane writes a flag into mapped pinned memory that the host spins on, (c) the same flag
-// written by hipStreamWriteValue32 behind the kernel, (d) atls_seal /
+// written by hipStreamWriteValue32 behind the kernel, (d) a one-key install waited for by a stream sync
+// and by atls_engine_sync, (e) atls_seal /
 // atls_open of one record (ChaCha20-Poly1305 and AES-128-GCM, 1,537 and 16,385 B). Prints JSON.
 // Build: hipcc --offload-arch=gfx950 -O2 -Iinclude tools/single_call_floor.hip -Lanothertls_amd -latls
 #include <hip/hip_runtime.h>
@@ -113,6 +114,13 @@ int main() {
       (void)hipStreamSynchronize(es);
     }, 2000);
     printf("%s\"aes%d_update1_stream_sync_us\": %.1f", kl == 16 ? ", " : ", ", kl * 8, up);
+    // the same through the engine's own wait (atls_engine_sync: a completion flag in mapped memory)
+    const double upe = median_us([&] {
+      slot = (slot + 1) % 64;
+      if (atls_update_keys(e, slot, &ks[slot], 1)) abort();
+      if (atls_engine_sync(e)) abort();
+    }, 2000);
+    printf(", \"aes%d_update1_engine_sync_us\": %.1f", kl * 8, upe);
     atls_engine_destroy(e);
   }
   std::vector<uint8_t> key(32, 7), iv(12, 1), aad = {0x17, 3, 3, 0x06, 0x11}, tag(16);
