@@ -88,7 +88,7 @@ struct DevBuf {
 }  // namespace
 
 #ifndef ATLS_SYNC_FLAG_DEFAULT
-#define ATLS_SYNC_FLAG_DEFAULT 0  // 1: synchronous returns wait on the sync-flag kernel (finish); env ATLS_SYNC_FLAG overrides
+#define ATLS_SYNC_FLAG_DEFAULT 1  // synchronous returns wait on the sync-flag kernel (finish); env ATLS_SYNC_FLAG=0: stream sync
 #endif
 struct atls_engine {
   int device = 0;
