@@ -148,6 +148,9 @@ int atls_open(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t*
 /* ---- Engine ---------------------------------------------------------------------------- */
 atls_engine* atls_engine_create(int device); /* NULL if the device is unusable */
 void atls_engine_destroy(atls_engine* e);
+/* Wait until everything enqueued on the engine has finished; reports a descriptor a NO_SYNC batch refused.
+ * Waits on a completion flag a one-lane kernel writes into mapped memory (env ATLS_SYNC_FLAG=0: a stream
+ * synchronisation instead). */
 int atls_engine_sync(atls_engine* e);
 /* HIP stream the engine launches on (hipStream_t as void*), for callers that time or order work.
  * Work of ATLS_FLAG_LAZY_JOIN batches is on it only after atls_engine_join. */
