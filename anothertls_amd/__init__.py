@@ -72,6 +72,7 @@ _lib.atls_multi_set_keys.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32]
 _lib.atls_multi_seal_batch.argtypes = _lib.atls_seal_batch.argtypes
 _lib.atls_multi_open_batch.argtypes = _lib.atls_open_batch.argtypes
 _lib.atls_partition.restype = None
+_lib.atls_clock_probe.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32, _c.c_uint32, _c.c_uint32, _c.c_void_p]
 _lib.atls_partition.argtypes = [_c.c_void_p, _c.c_uint32, _c.c_int, _c.c_uint32, _c.c_void_p]
 
 
@@ -294,6 +295,11 @@ class Engine:
     def set_keys(self, keys):
         keys = np.ascontiguousarray(keys, dtype=KEY_DTYPE)
         _check(_lib.atls_set_keys(self._e, keys.ctypes.data, len(keys)))
+
+    def clock_probe(self, out, wgs=8, delay_us=0, spin_us=1000, stream=None):
+        """Enqueue the shader-clock probe (atls_clock_probe): `out` a device tensor of >= 2 * wgs int64, on
+        `stream` (a hipStream_t handle; None = the engine's stream). SCLK MHz = 100 * out[2w] / out[2w+1]."""
+        _check(_lib.atls_clock_probe(self._e, stream, int(wgs), int(delay_us), int(spin_us), _ptr(out)))
 
     def update_keys(self, first, keys):
         """Install key slots [first, first + len(keys)), keeping the other slots."""

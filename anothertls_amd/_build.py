@@ -6,7 +6,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libatls.so")
-SOURCES = ["engine.cpp", "keysetup.hip", "plan.hip", "gcm.hip", "chacha.hip", "hkdf.hip", "aes_block.hip", "stream.cpp", "multi.cpp"]
+SOURCES = ["engine.cpp", "keysetup.hip", "plan.hip", "gcm.hip", "chacha.hip", "hkdf.hip", "aes_block.hip", "diag.hip", "stream.cpp", "multi.cpp"]
 ARCH = os.environ.get("ATLS_OFFLOAD_ARCH", "gfx950")
 
 

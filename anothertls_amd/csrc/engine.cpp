@@ -40,6 +40,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
                                const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
 extern "C" size_t atls_group_hdr_offset(uint32_t n_slots);
+extern "C" int atls_launch_clock_probe(uint32_t wgs, uint32_t delay_us, uint32_t spin_us, uint64_t* out, hipStream_t s);
 extern "C" int atls_launch_sync_flag(const uint32_t* err, uint32_t* out, uint32_t val, hipStream_t s);
 extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t n_slots, const atls_rec* d,
                                       const uint8_t* bytes, uint32_t nbytes, uint32_t tag_off, uint8_t* out,
@@ -1170,6 +1171,13 @@ int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* 
     return finish(e, flags & ~ATLS_FLAG_NO_SYNC, true);
   }
   return finish(e, flags);
+}
+
+int atls_clock_probe(atls_engine* e, void* stream, uint32_t wgs, uint32_t delay_us, uint32_t spin_us, uint64_t* out) {
+  if (!e) return ATLS_INTERNAL_ERROR;
+  if (!out || wgs == 0 || wgs > 1024 || delay_us > 10000000u || spin_us > 10000000u) return ATLS_ILLEGAL_PARAMETER;
+  if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
+  return atls_launch_clock_probe(wgs, delay_us, spin_us, out, stream ? (hipStream_t)stream : e->stream);
 }
 
 int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_t in[16], uint8_t out[16]) {

@@ -1120,8 +1120,34 @@ __device__ __forceinline__ void gcm_one(const GcmArgs& A, uint32_t r, uint32_t l
 // count (a kernel holds only that count's round keys); the waves take the records of that round
 // count's work list (plan.hip, longest first) round-robin, spread over the workgroups, or a key-grouped direct batch's lane
 // groups from a work counter.
+// In-kernel clock (diagnostic build -DATLS_CLK_STAMPS, MI355X_MICROARCH.md "DVFS give-back" item 6): every
+// wave adds its s_memtime and s_memrealtime spans over the whole kernel body to g_clk_stamps (read back and
+// reset by atls_debug_clk_stamps); the clock is 100 MHz x sum(shader ticks) / sum(constant ticks). Checks
+// atls_clock_probe, which reads the same counters from a wave beside the kernel (tools/clock_check.py).
+#ifdef ATLS_CLK_STAMPS
+__device__ unsigned long long g_clk_stamps[4];
+#endif
+template <bool OPEN, int kWaves, int NR>
+__device__ __forceinline__ void gcm_kernel_body(const GcmArgs& A);
+
 template <bool OPEN, int kWaves, int NR>
 __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
+#ifdef ATLS_CLK_STAMPS
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  gcm_kernel_body<OPEN, kWaves, NR>(A);
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&g_clk_stamps[0], t1 - t0);
+    atomicAdd(&g_clk_stamps[1], r1 - r0);
+    atomicAdd(&g_clk_stamps[2], 1ull);
+  }
+#else
+  gcm_kernel_body<OPEN, kWaves, NR>(A);
+#endif
+}
+
+template <bool OPEN, int kWaves, int NR>
+__device__ __forceinline__ void gcm_kernel_body(const GcmArgs& A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   // T0 (1 KiB) through the (still unused) GHASH area: one global load per thread instead of a
   // dependent load per LDS word of the 64 KiB replicated tables
@@ -1347,7 +1373,26 @@ extern "C" unsigned atls_build_flags(void) {
 #ifdef ATLS_TT_STAMPS
   f |= ATLS_BUILD_TT_STAMPS;
 #endif
+#ifdef ATLS_CLK_STAMPS
+  f |= ATLS_BUILD_CLK_STAMPS;
+#endif
   return f;
+}
+
+// Debug: copy out (and reset) the in-kernel clock sums of a -DATLS_CLK_STAMPS build: {sum of shader-clock
+// ticks, sum of 100 MHz ticks, waves}; -1 otherwise.
+extern "C" int atls_debug_clk_stamps(unsigned long long* out) {
+#ifdef ATLS_CLK_STAMPS
+  unsigned long long h[4], z[4] = {};
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(atls::g_clk_stamps), sizeof(h)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(atls::g_clk_stamps), z, sizeof(z)) != hipSuccess) return -1;
+  for (int i = 0; i < 4; i++) out[i] = h[i];
+  return 0;
+#else
+  (void)out;
+  return -1;
+#endif
 }
 
 // Debug: copy out (and reset) the phase timers of a -DATLS_TT_STAMPS build; -1 otherwise.

@@ -351,6 +351,66 @@ def copy_probe(d_in, d_out, min_ms):
     return 2 * nbytes * reps / (total_ms * 1e-3) / 1e9
 
 
+# LDS-array roofline of the AES-GCM record kernels. The static instruction mix per 16-byte
+# block: AES-CTR by two-table T-table rounds with counter-mode caching -- 1 + 4 + 16 x (NR - 2) conflict-free
+# ds_read_b32 (133 for AES-128, 165 for AES-192, 197 for AES-256) -- and one GHASH product by the 4-bit table,
+# 32 ds_read_b128. A wave-instruction serves 64 blocks and costs 2 (b32) / 4 (b128) LDS-array cycles
+# (MI355X_MICROARCH.md §LDS table). A record of AEAD length L has ceil(L/16) + 1 AES blocks (its counter
+# blocks and E_K(J0)) and ceil(L/16) + 2 GHASH products (one AAD block, the ciphertext, the length block).
+LDS_B32_PER_AES_BLOCK = {10: 133, 12: 165, 14: 197}
+LDS_CYCLES_B32, LDS_CYCLES_B128, GHASH_B128_PER_BLOCK = 2, 4, 32
+
+
+def lds_cycles_per_launch(batch):
+    """Algorithmic LDS-array CU-cycles of one seal launch over an AES-GCM batch (None unless every record is
+    AES-GCM: a mixed batch's launch interval also holds the VALU-bound ChaCha20-Poly1305 kernel): the
+    per-block static mix above times the blocks; table builds, lane combines and the lanes idle in a record's
+    last step are not counted (the measured SQ_LDS_IDX_ACTIVE includes them)."""
+    keys, recs = batch["keys"], batch["recs"]
+    suite = keys["suite"][recs["key_slot"]]
+    aes = suite != 0x1303
+    if not aes.all():
+        return None
+    L = recs["len"][aes].astype(np.int64) + 1  # TLS: content || type
+    nr = np.where(keys["key_len"][recs["key_slot"][aes]] == 16, 10, np.where(keys["key_len"][recs["key_slot"][aes]] == 24, 12, 14))
+    b32 = np.vectorize(LDS_B32_PER_AES_BLOCK.get)(nr)
+    blocks = (L + 15) // 16
+    cyc = (blocks + 1) * b32 * LDS_CYCLES_B32 + (blocks + 2) * GHASH_B128_PER_BLOCK * LDS_CYCLES_B128
+    return float(cyc.sum()) / 64.0
+
+
+def clock_pass(eng, dev, launch, n_launch, kern_ms):
+    """The shader clock of `n_launch` more back-to-back launches (outside any timed region): the clock probe
+    (atls_clock_probe, 16 one-wave workgroups on a second stream) sleeps through the first fifth of them and
+    reads s_memtime against s_memrealtime over the next half. Returns the median MHz over the workgroups."""
+    side = torch.cuda.Stream(device=dev)
+    wgs = 16
+    out = torch.zeros(2 * wgs, dtype=torch.int64, device=dev)
+    span_us = n_launch * kern_ms * 1e3
+    torch.cuda.synchronize(dev)
+    eng.clock_probe(out, wgs=wgs, delay_us=int(0.2 * span_us), spin_us=max(20, int(0.5 * span_us)),
+                    stream=side.cuda_stream)
+    for _ in range(n_launch):
+        launch()
+    eng.sync()
+    torch.cuda.synchronize(dev)
+    o = out.cpu().numpy().reshape(wgs, 2).astype(np.float64)
+    return float(np.median(100.0 * o[:, 0] / np.maximum(o[:, 1], 1)))
+
+
+def lds_roofline(batch, kern_ms, sclk_mhz, cus):
+    """roofline.lds: the launch's algorithmic LDS-array cycles at the measured clock on every CU, as a
+    fraction of the measured launch time."""
+    cyc = lds_cycles_per_launch(batch)
+    if cyc is None or not sclk_mhz:
+        return None
+    t_ms = cyc / cus / (sclk_mhz * 1e3)
+    return {"bound": "lds", "cycles_per_launch": round(cyc), "sclk_MHz": round(sclk_mhz, 1), "cus": cus,
+            "t_min_ms": round(t_ms, 4), "kernel_ms": round(kern_ms, 4), "frac": round(t_ms / kern_ms, 4),
+            "per_block": "AES-CTR 1+4+16(NR-2) ds_read_b32 x 2 cyc + GHASH 32 ds_read_b128 x 4 cyc, per 64 blocks",
+            "clock": "atls_clock_probe beside the same launches (s_memtime / s_memrealtime, median of 16 waves)"}
+
+
 def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_slots=None, keep=False,
             settle_ms=0.0):
     """This rank's shard of config `name`, device-resident: `steps` timed seals (barrier + sync on both
@@ -407,6 +467,11 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
     m = {"batch": batch, "n": n, "wall": wall, "kern_ms": kern_ms, "payload": payload, "alg_bytes": alg_bytes,
          "achieved": achieved, "value": dist.whole_job_rate(payload, steps, wall, world), "flags": flags,
          "stream": stream, "sync": sync, "copy_gbps": copy_gbps}
+    if lds_cycles_per_launch(batch) is not None:
+        # the clock of `steps` more of the same seals, after the timed region (the LDS roofline is in cycles)
+        m["sclk_mhz"] = clock_pass(eng, dev, lambda: eng.seal_batch(p_recs, p_in, p_aux, p_out, p_tags, flags=flags, n=n),
+                                   steps, kern_ms)
+        m["lds"] = lds_roofline(batch, kern_ms, m["sclk_mhz"], torch.cuda.get_device_properties(dev).multi_processor_count)
 
     # ---- the decrypt half (Gcm::decrypt, gcm.rs:142-157, via record.rs:201-240) over the records
     # just sealed: same records, same bytes per record (read L + 16-byte tag, write L) ----
@@ -460,7 +525,8 @@ def config_summary(name, m, steps):
             "frac": round(m["achieved"] / HBM_PEAK_GBPS, 4), "alg_bytes_per_launch": m["alg_bytes"],
             "suite": suite if isinstance(suite, str) else suite.name,
             "aead_bytes_per_record": (clen + 1) if isinstance(clen, int) else "content U{64..16384}+1",
-            "open": {k: v for k, v in m["open"].items() if k != "what"}}
+            "open": {k: v for k, v in m["open"].items() if k != "what"},
+            **({"lds": {k: v for k, v in m["lds"].items() if k not in ("per_block", "clock")}} if m.get("lds") else {})}
 
 
 def main():
@@ -513,7 +579,12 @@ def main():
         n_sus = max(1, int(args.sustain_s * 1e3 / max(kern_ms, 1e-3)))
         s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         p_recs, p_in, p_aux, p_out, p_tags = (t.data_ptr() for t in (m["d_recs"], d_in, d_aux, d_out, d_tags))
+        probe = torch.zeros(32, dtype=torch.int64, device=dev)
+        side = torch.cuda.Stream(device=dev)
         eng.join()
+        sync()
+        span_us = n_sus * kern_ms * 1e3  # the probe reads the clock over the middle of the leg
+        eng.clock_probe(probe, wgs=16, delay_us=int(0.3 * span_us), spin_us=int(0.4 * span_us), stream=side.cuda_stream)
         s0.record(stream)
         for _ in range(n_sus):
             eng.seal_batch(p_recs, p_in, p_aux, p_out, p_tags, flags=flags, n=n)
@@ -521,11 +592,16 @@ def main():
         s1.record(stream)
         sync()
         sus_ms = s0.elapsed_time(s1) / n_sus
+        o = probe.cpu().numpy().reshape(16, 2).astype(np.float64)
+        sus_sclk = float(np.median(100.0 * o[:, 0] / np.maximum(o[:, 1], 1)))
         sus_ach = alg_bytes / (sus_ms * 1e-3) / 1e9
         sustained = {"seconds": round(sus_ms * n_sus / 1e3, 2), "launches": n_sus, "kernel_ms": round(sus_ms, 4),
                      "GiBps_per_gpu": round(payload / (sus_ms * 1e-3) / 2**30, 3),
-                     "frac": round(sus_ach / HBM_PEAK_GBPS, 4),
+                     "frac": round(sus_ach / HBM_PEAK_GBPS, 4), "sclk_MHz": round(sus_sclk, 1),
                      "what": "rank 0's seals back to back after the timed steps (HIP events); not the reported value"}
+        lds_sus = lds_roofline(batch, sus_ms, sus_sclk, torch.cuda.get_device_properties(dev).multi_processor_count)
+        if lds_sus:
+            sustained["lds_frac"] = lds_sus["frac"]
 
     result = None
     if rank == 0:
@@ -556,7 +632,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                          "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes,
-                         "copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(achieved / copy_gbps, 4)},
+                         "copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(achieved / copy_gbps, 4),
+                         "lds": m.get("lds")},
             "open": m["open"],
         }
         if sustained:
@@ -666,6 +743,13 @@ def main():
             mm = measure(name, eng, dev, rank, world, min(steps, 5), min(warmup, 1), not args.no_lazy_join,
                          records=workload.CONFIGS[name][1], settle_ms=args.settle_ms)
             cfgs[name + " (whole batch, 1 GPU)"] = config_summary(name, mm, min(steps, 5))
+            del mm
+            torch.cuda.empty_cache()
+            # C5 likewise: the whole 256 Ki-record mixed batch (2.16 GB each way) in one planned launch
+            name = "c5_mixed_256Ki_x_64B-16KiB"
+            mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join,
+                         records=workload.CONFIGS[name][1], settle_ms=args.settle_ms)
+            cfgs[name + " (whole batch, 1 GPU)"] = config_summary(name, mm, steps)
             del mm
             torch.cuda.empty_cache()
         if rank == 0:

@@ -266,6 +266,15 @@ long atls_sb_recv(atls_stream_batch* sb, int conn, size_t max_bytes); /* bytes r
 long atls_sb_open_pending(atls_stream_batch* sb);                /* records opened */
 int atls_sb_read(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size_t* out_len);
 
+/* Diagnostic (no reference counterpart): the shader clock the device runs at under the current load, for
+ * rooflines counted in cycles. Enqueues wgs (1..1024) one-wave workgroups on `stream`
+ * (hipStream_t as void*; NULL = the engine's stream). Each sleeps delay_us microseconds of the 100 MHz
+ * constant clock, then writes {shader-clock ticks, constant-clock ticks} over spin_us more to out[2w],
+ * out[2w+1] (device memory, 16 B per workgroup): SCLK = 100 MHz x out[2w] / out[2w+1]. The probe uses no
+ * LDS, so on a second stream it runs beside a batch's kernels and samples their clock. delay_us and
+ * spin_us are each at most 10,000,000 (else ATLS_ILLEGAL_PARAMETER). No host wait. */
+int atls_clock_probe(atls_engine* e, void* stream, uint32_t wgs, uint32_t delay_us, uint32_t spin_us, uint64_t* out);
+
 /* Library info: ABI version and the device arch the code objects were built for ("gfx950"). */
 int atls_abi_version(void);
 const char* atls_device_arch(void);
@@ -273,7 +282,8 @@ const char* atls_device_arch(void);
  * experiments that drop work (ATLS_DBG_*) give wrong results; tests assert this is 0. */
 enum {
   ATLS_BUILD_DBG_SKIP = 1u, ATLS_BUILD_DBG_SHARED_GHASH = 2u, ATLS_BUILD_GHASH_W = 4u,
-  ATLS_BUILD_NO_CTR_CACHE = 8u, ATLS_BUILD_GHASH_ROT = 16u, ATLS_BUILD_TT_STAMPS = 32u
+  ATLS_BUILD_NO_CTR_CACHE = 8u, ATLS_BUILD_GHASH_ROT = 16u, ATLS_BUILD_TT_STAMPS = 32u,
+  ATLS_BUILD_CLK_STAMPS = 64u
 };
 unsigned atls_build_flags(void);
 
