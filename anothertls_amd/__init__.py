@@ -68,6 +68,9 @@ _lib.atls_multi_create.argtypes = [_c.c_void_p, _c.c_int]
 _lib.atls_multi_destroy.argtypes = [_c.c_void_p]
 _lib.atls_multi_devices.argtypes = [_c.c_void_p]
 _lib.atls_multi_uses_rccl.argtypes = [_c.c_void_p]
+_lib.atls_multi_rccl_version.argtypes = [_c.c_void_p]
+_lib.atls_multi_max_message.argtypes = [_c.c_void_p]
+_lib.atls_multi_max_message.restype = _c.c_size_t
 _lib.atls_multi_set_keys.argtypes = [_c.c_void_p, _c.c_void_p, _c.c_uint32]
 _lib.atls_multi_seal_batch.argtypes = _lib.atls_seal_batch.argtypes
 _lib.atls_multi_open_batch.argtypes = _lib.atls_open_batch.argtypes
@@ -374,6 +377,16 @@ class MultiEngine:
     @property
     def uses_rccl(self):
         return bool(_lib.atls_multi_uses_rccl(self._m))
+
+    @property
+    def rccl_version(self):
+        """ncclGetVersion of the RCCL in use (e.g. 22606 = 2.26.6), 0 without RCCL."""
+        return int(_lib.atls_multi_rccl_version(self._m))
+
+    @property
+    def max_message(self):
+        """Largest RCCL point-to-point message in bytes (0 without RCCL)."""
+        return int(_lib.atls_multi_max_message(self._m))
 
     def close(self):
         if self._m:

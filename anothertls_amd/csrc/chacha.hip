@@ -734,7 +734,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 
 // One group of G lanes seals / opens the record at work-list position q (direct batches: the
 // kernel validates the descriptor itself).
-template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G == 64 ? 1 : 0, bool STAGE = false>
+template <bool OPEN, int G, bool LATE, bool CARRY = false, int PRE = G >= 64 ? 1 : 0, bool STAGE = false>
 __device__ __forceinline__ void chacha_group(const ChArgs& A, const WorkList& W, uint32_t q, uint32_t cnt, int gl,
                                              lds_uint4* lds = nullptr) {
   if (q >= cnt) return;

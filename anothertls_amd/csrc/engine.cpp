@@ -16,6 +16,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -186,13 +187,23 @@ int finish(atls_engine* e, uint32_t flags, bool host_copies = false) {
   if (join_pending(e)) return ATLS_INTERNAL_ERROR;
   uint32_t err = 0;
   if (!host_copies && sync_flag_ready(e)) {
-    // everything before it on the engine stream has finished once the flag reads v; a stream that ends
-    // without it (a fault) is reported by hipStreamQuery, checked every few thousand spins
+    // everything before it on the engine stream has finished once the flag reads v. The host spins for at
+    // most kSpinUs (the small-call latency win), then blocks in hipStreamSynchronize, so a long
+    // batch does not hold a core; a stream that ends without the flag (a fault) is reported by
+    // hipStreamQuery, checked every few thousand spins, or by the synchronisation
+    constexpr int64_t kSpinUs = 100;
     const uint32_t v = ++e->sync_val;
     __atomic_store_n(&e->sync_h[0], v - 1u, __ATOMIC_RELEASE);
     if (atls_launch_sync_flag((const uint32_t*)e->err.p, e->sync_d, v, e->stream)) return ATLS_INTERNAL_ERROR;
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t i = 1;; i++) {
       if (__atomic_load_n(&e->sync_h[0], __ATOMIC_ACQUIRE) == v) break;
+      if ((i & 255) == 0 && std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0)
+                                    .count() > kSpinUs) {
+        if (hipStreamSynchronize(e->stream) != hipSuccess) return ATLS_INTERNAL_ERROR;
+        if (__atomic_load_n(&e->sync_h[0], __ATOMIC_ACQUIRE) != v) return ATLS_INTERNAL_ERROR;
+        break;
+      }
       if ((i & 4095) == 0) {
         const hipError_t q = hipStreamQuery(e->stream);
         if (q == hipSuccess) {
@@ -305,8 +316,16 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
     e->down = nullptr;
     return ATLS_INTERNAL_ERROR;
   }
-  bool pitched = n > 1;
+  // Output layouts: gapless (every record's output starts where the previous one's ends -- WIRE seals
+  // packed back to back, the socket path's case) comes back as one linear copy per chunk, with nothing
+  // staged in; a fixed pitch with gaps (TLS seals in 16-byte slots, C2 / C4) by a 2-D copy that skips the
+  // gaps -- when the pitch is a multiple of 16: a 2-D copy of 16,406-byte rows ran at 1.7 GB/s against 32
+  // for the same bytes linear (tools/host_batch_probe.py, profiles/r05/host_batch_probe*.log); anything
+  // else stages the chunk's output range in and out.
+  bool gapless = true;
+  for (uint32_t i = 1; i < n && gapless; i++) gapless = recs[i].out_off == recs[i - 1].out_off + olen(recs[i - 1]);
   const size_t pitch = n > 1 ? (size_t)(recs[1].out_off - recs[0].out_off) : 0, width = olen(recs[0]);
+  bool pitched = n > 1 && !gapless && pitch % 16 == 0;
   for (uint32_t i = 1; i < n && pitched; i++)
     pitched = olen(recs[i]) == width && recs[i].out_off == recs[0].out_off + i * pitch;
   hipStream_t ks = e->stream, up = e->up, down = e->down;
@@ -363,7 +382,7 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
     if (open && tags_in && hipMemcpyAsync(d_tags + 16 * (size_t)a, tags_in + 16 * (size_t)a, 16 * (size_t)cnt,
                                hipMemcpyHostToDevice, up) != hipSuccess)
       return fail(ATLS_INTERNAL_ERROR);
-    if (!zo && !pitched && out_hi > out_lo &&
+    if (!zo && !pitched && !gapless && out_hi > out_lo &&
         hipMemcpyAsync(d_out + out_lo, (uint8_t*)out + out_lo, out_hi - out_lo, hipMemcpyHostToDevice, up) != hipSuccess)
       return fail(ATLS_INTERNAL_ERROR);
     if (hipEventRecord(uploaded, up) != hipSuccess || hipStreamWaitEvent(ks, uploaded, 0) != hipSuccess)
@@ -568,7 +587,9 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     if (lazy) ps.pending = true;
     else if (hipStreamWaitEvent(s, ps.side_done, 0) != hipSuccess) return ATLS_INTERNAL_ERROR;
   }
-  if (zc) return finish(e, flags & ~ATLS_FLAG_NO_SYNC);  // host buffers: the batch ends before the call returns
+  // host buffers read and written in place: the batch ends before the call returns, by a stream synchronisation
+  // (the kernels' stores to page-locked host memory are covered by the stream's completion)
+  if (zc) return finish(e, flags & ~ATLS_FLAG_NO_SYNC, true);
   if (!dev_ptrs) {
     if (out_end && hipMemcpyAsync(out, e->out.p, out_end, hipMemcpyDeviceToHost, s) != hipSuccess)
       return ATLS_INTERNAL_ERROR;

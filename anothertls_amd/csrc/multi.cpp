@@ -28,6 +28,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -52,6 +53,9 @@ struct Rccl {
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclGetVersion) get_version = nullptr;
+  int version = 0;          // NCCL_VERSION_CODE of the library actually loaded (e.g. 22606 for 2.26.6)
+  const char* path = "";    // its file (dladdr)
   bool ok = false;
 };
 static_assert(std::is_same<decltype(Rccl::send), ncclResult_t (*)(const void*, size_t, ncclDataType_t, int, ncclComm_t,
@@ -83,7 +87,11 @@ const Rccl& rccl() {
     resolve(h, "ncclSend", r.send);
     resolve(h, "ncclRecv", r.recv);
     resolve(h, "ncclGetErrorString", r.error_string);
-    r.ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.send && r.recv;
+    resolve(h, "ncclGetVersion", r.get_version);
+    r.ok = r.comm_init_all && r.comm_destroy && r.group_start && r.group_end && r.send && r.recv && r.get_version;
+    if (r.ok && r.get_version(&r.version) != ncclSuccess) r.version = 0;
+    Dl_info info;
+    if (r.ok && dladdr(reinterpret_cast<void*>(r.send), &info) && info.dli_fname) r.path = info.dli_fname;
   });
   return r;
 }
@@ -135,17 +143,35 @@ struct atls_multi {
   // then goes through exactly the RCCL branch of run_device on a one-GPU box (tests).
   bool rccl_self = false;
   size_t xfer_chunk = ~size_t(0);  // largest RCCL message (multi_xfer_chunk() at creation)
+  int rccl_version = 0;            // of the loaded library (0 without RCCL)
   std::mutex mu;
 };
 
 namespace {
 
-// Largest RCCL point-to-point message (ATLS_MULTI_CHUNK_MB when the multi engine is created, default
-// 1024 MiB; 0 = none): larger ranges go in several messages.
-size_t multi_xfer_chunk() {
+// Largest RCCL point-to-point message: ATLS_MULTI_CHUNK_MB when the multi engine is created (0 = none),
+// else 1024 MiB. RCCL 2.26.6 (the library PyTorch ships, which this process resolves librccl.so.1 to
+// once torch is loaded) returns wrong bytes past 2^30 of a self send / recv of 2 GiB
+// (profiles/r04/multi_diag.log); tools/rccl_p2p_probe brackets the threshold per library
+// (profiles/r05/rccl_p2p_probe_*.log). 1 GiB pieces are what every tested message size
+// below the threshold is, for every version seen.
+constexpr size_t kRcclSafePiece = size_t(1) << 30;
+size_t multi_xfer_chunk(int version) {
+  (void)version;  // one cap for every library version measured so far
   const char* e = std::getenv("ATLS_MULTI_CHUNK_MB");
-  const long mb = e ? std::atol(e) : 1024;
+  if (!e) return kRcclSafePiece;
+  const long mb = std::atol(e);
   return mb > 0 ? (size_t)mb << 20 : ~size_t(0);
+}
+
+// Once per process: which RCCL the multi engines use and the message cap.
+void log_rccl(const Rccl& R, size_t cap) {
+  static std::once_flag once;
+  std::call_once(once, [&] {
+    std::fprintf(stderr, "anothertls_amd: RCCL %d.%d.%d (%s), point-to-point messages capped at %zu MiB\n",
+                 R.version / 10000, (R.version / 100) % 100, R.version % 100, R.path,
+                 cap == ~size_t(0) ? (size_t)0 : cap >> 20);
+  });
 }
 
 // Wait for everything queued for this batch (engine streams, transfer streams), and clear the
@@ -469,7 +495,9 @@ atls_multi* atls_multi_create(const int* devices, int n_devices) {
     }
     m->use_rccl = true;
     m->rccl_self = self;
-    m->xfer_chunk = multi_xfer_chunk();
+    m->rccl_version = R.version;
+    m->xfer_chunk = multi_xfer_chunk(R.version);
+    log_rccl(R, m->xfer_chunk);
   }
   return m;
 }
@@ -492,6 +520,8 @@ void atls_multi_destroy(atls_multi* m) {
 
 int atls_multi_devices(const atls_multi* m) { return m ? (int)m->parts.size() : 0; }
 int atls_multi_uses_rccl(const atls_multi* m) { return m && m->use_rccl ? 1 : 0; }
+int atls_multi_rccl_version(const atls_multi* m) { return m && m->use_rccl ? m->rccl_version : 0; }
+size_t atls_multi_max_message(const atls_multi* m) { return m && m->use_rccl ? m->xfer_chunk : 0; }
 
 int atls_multi_set_keys(atls_multi* m, const atls_key* keys, uint32_t n) {
   if (!m) return ATLS_INTERNAL_ERROR;

@@ -12,14 +12,14 @@ constexpr int kDecodeError = 51;  // TlsError::DecodeError, net/alert.rs
 
 inline bool record_type_ok(uint32_t b) { return b == 0 || (b >= 20 && b <= 23); }  // RecordType::new, record.rs:23-32
 
-// Moves the whole records at the front of rx[0, n) to wire (appending each record's offset in
-// wire to offs) and returns the bytes consumed. A partial record at the end waits for more
-// bytes (the reference has a todo!() there, stream.rs:106-108). A complete header whose type is
-// not a RecordType, or that frames fewer bytes than a tag (the reference's fragment[..len-16]
-// would underflow, record.rs:208), stops the split with err = DecodeError. The reference's bounds
-// check is 2 + len (record.rs:88); this reads only whole 5 + len byte records.
-inline size_t split_records(const uint8_t* rx, size_t n, std::vector<uint8_t>& wire, std::vector<uint32_t>& offs,
-                            int& err) {
+// The whole records at the front of rx[0, n): appends each record's offset (its position in rx plus
+// `base`) to offs and returns the bytes they span; the bytes stay where they are (the batched socket
+// path opens them in place). A partial record at the end waits for more bytes (the reference has a
+// todo!() there, stream.rs:106-108). A complete header whose type is not a RecordType, or that frames
+// fewer bytes than a tag (the reference's fragment[..len-16] would underflow, record.rs:208), stops the
+// scan with err = DecodeError. The reference's bounds check is 2 + len (record.rs:88); this takes only
+// whole 5 + len byte records.
+inline size_t scan_records(const uint8_t* rx, size_t n, size_t base, std::vector<uint32_t>& offs, int& err) {
   size_t pos = 0;
   while (n - pos >= 5) {
     const uint8_t* h = rx + pos;
@@ -29,11 +29,18 @@ inline size_t split_records(const uint8_t* rx, size_t n, std::vector<uint8_t>& w
       err = kDecodeError;
       break;
     }
-    offs.push_back((uint32_t)wire.size());
-    wire.insert(wire.end(), h, h + 5 + len);
+    offs.push_back((uint32_t)(base + pos));
     pos += 5 + len;
   }
   return pos;
+}
+
+// As scan_records, with the whole records moved (appended) to wire and their offsets in wire.
+inline size_t split_records(const uint8_t* rx, size_t n, std::vector<uint8_t>& wire, std::vector<uint32_t>& offs,
+                            int& err) {
+  const size_t used = scan_records(rx, n, wire.size(), offs, err);
+  wire.insert(wire.end(), rx, rx + used);
+  return used;
 }
 
 }  // namespace atls_split

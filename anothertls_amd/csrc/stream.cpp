@@ -15,16 +15,34 @@
 // Divergence (documented): writes longer than 2^14 bytes are fragmented into 2^14-byte records
 // (RFC 8446 §5.1); the reference emits one over-long record. Writes up to 2^14 bytes produce the
 // reference's wire bytes.
+//
+// Throughput (round 5): the host work around the device batch is copies and socket
+// calls, so the batch keeps them few and spreads them over worker threads (atls_sb_set_threads):
+//   * a write is copied once, into the batch's page-locked input arena the seal batch reads;
+//   * flush sends the connections' slices of the page-locked wire buffer from T threads;
+//   * atls_sb_recv_all receives on every connection from T threads, straight into each connection's
+//     receive buffer, where the whole records are found in place (record_split.h scan_records);
+//   * atls_sb_open_pending gathers the connections' whole records into the page-locked wire buffer,
+//     opens them in one batch and hands each connection its plaintexts, both from T threads;
+//   * a connection's opened records sit behind its own lock, so readers of different connections
+//     (atls_sb_read / atls_sb_read_ready) copy out in parallel.
 #include <hip/hip_runtime.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <sys/types.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cerrno>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/atls.h"
@@ -35,18 +53,22 @@ namespace {
 constexpr size_t kMaxFragment = size_t(1) << 14;  // RFC 8446 §5.1
 constexpr int kUnexpectedMessage = 10;            // TlsError::UnexpectedMessage, alert.rs:22
 constexpr int kBrokenPipe = 254;                  // TlsError::BrokenPipe, alert.rs:44
+constexpr size_t kRecvChunk = size_t(256) << 10;  // room made in a receive buffer per recv call
+constexpr size_t kRxMax = size_t(1) << 31;        // unopened bytes per connection (record offsets are u32)
+constexpr int kMaxThreads = 64;
 
-
-// Grow-only page-locked host buffer: the engine's copies from it run at full PCIe speed.
+// Grow-only page-locked host buffer: the engine's copies from it run at full PCIe speed. keep: bytes
+// [0, keep) survive a growth (the write arena fills across several writes).
 struct Pinned {
   uint8_t* p = nullptr;
   size_t cap = 0;
-  bool reserve(size_t n) {
+  bool reserve(size_t n, size_t keep = 0) {
     if (n <= cap) return true;
     size_t c = cap ? cap : (size_t(1) << 20);
     while (c < n) c *= 2;
     void* q = nullptr;
     if (hipHostMalloc(&q, c, hipHostMallocDefault) != hipSuccess) return false;
+    if (p && keep) std::memcpy(q, p, keep);
     if (p) (void)hipHostFree(p);
     p = (uint8_t*)q;
     cap = c;
@@ -62,16 +84,29 @@ struct Record {
   std::vector<uint8_t> data;
 };
 
+struct Queued {  // a record waiting for the next flush; its content is in the batch's input arena
+  size_t in_off;
+  uint32_t len;
+  uint8_t type;
+};
+
+struct Inbox {  // opened records of one connection (its own lock: readers of different connections run in parallel)
+  std::mutex mu;
+  std::deque<Record> q;
+  int err = 0;  // the connection's error, visible to readers once every record before it was handed over
+};
+
 struct Conn {
   int fd = -1;
   uint32_t wslot = 0, rslot = 0;  // key slots: write key, read key
   uint64_t wseq = 0, rseq = 0;
-  int err = 0;                    // TlsError that ended the connection
-  std::vector<Record> out;        // queued for the next flush
-  std::vector<uint8_t> rx;        // received bytes not yet split into records
-  std::vector<uint8_t> wire;      // whole received records waiting for open_pending
-  std::vector<uint32_t> offs;     // their offsets in wire
-  std::deque<Record> inbox;       // opened records
+  int err = 0;                    // TlsError that ended the connection (batch side)
+  bool eof = false;               // the peer closed (recv returned 0)
+  std::vector<Queued> out;        // queued for the next flush
+  std::vector<uint8_t> rx;        // received bytes [0, rx_len); whole records at offs, scanned up to rx_done
+  size_t rx_len = 0, rx_done = 0;
+  std::vector<uint32_t> offs;
+  std::unique_ptr<Inbox> inbox{new Inbox};
 };
 
 bool send_all(int fd, const uint8_t* p, size_t n) {
@@ -79,6 +114,11 @@ bool send_all(int fd, const uint8_t* p, size_t n) {
     const ssize_t k = send(fd, p, n, MSG_NOSIGNAL);
     if (k < 0) {
       if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) {  // a non-blocking socket: wait until it drains
+        pollfd q{fd, POLLOUT, 0};
+        (void)poll(&q, 1, 1000);
+        continue;
+      }
       return false;
     }
     p += k;
@@ -87,10 +127,55 @@ bool send_all(int fd, const uint8_t* p, size_t n) {
   return true;
 }
 
-// Moves the whole records at the front of c.rx to c.wire (record_split.h, Record::from_raw checks).
-void split(Conn& c) {
-  const size_t pos = atls_split::split_records(c.rx.data(), c.rx.size(), c.wire, c.offs, c.err);
-  c.rx.erase(c.rx.begin(), c.rx.begin() + (std::ptrdiff_t)pos);
+// Finds the whole records among the received bytes not yet scanned (record_split.h).
+void scan(Conn& c) {
+  if (c.err) return;
+  c.rx_done += atls_split::scan_records(c.rx.data() + c.rx_done, c.rx_len - c.rx_done, c.rx_done, c.offs, c.err);
+}
+
+void append_rx(Conn& c, const uint8_t* data, size_t len) {
+  if (c.rx.size() < c.rx_len + len) c.rx.resize(std::max(c.rx_len + len, 2 * c.rx.size()));
+  std::memcpy(c.rx.data() + c.rx_len, data, len);
+  c.rx_len += len;
+}
+
+// Receives what the socket holds (non-blocking) straight into c.rx; returns the bytes received.
+size_t drain_socket(Conn& c) {
+  size_t got = 0;
+  while (!c.err && !c.eof) {
+    if (c.rx_len >= kRxMax) break;  // the owner must open before more is read
+    if (c.rx.size() < c.rx_len + kRecvChunk) c.rx.resize(std::max(c.rx_len + kRecvChunk, 2 * c.rx.size()));
+    const ssize_t k = recv(c.fd, c.rx.data() + c.rx_len, c.rx.size() - c.rx_len, MSG_DONTWAIT);
+    if (k > 0) {
+      c.rx_len += (size_t)k;
+      got += (size_t)k;
+      continue;
+    }
+    if (k == 0) c.eof = true;
+    else if (errno == EINTR) continue;
+    else if (errno != EAGAIN && errno != EWOULDBLOCK) c.err = kBrokenPipe;
+    break;
+  }
+  scan(c);
+  return got;
+}
+
+// fn(i) for i in [0, n) on up to `threads` threads (the caller's included), item i on thread i % T.
+template <typename F>
+void parallel(int threads, size_t n, F fn) {
+  const size_t T = std::min<size_t>((size_t)std::max(threads, 1), n);
+  if (T <= 1) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::vector<std::thread> ts;
+  ts.reserve(T - 1);
+  for (size_t t = 1; t < T; t++)
+    ts.emplace_back([&, t] {
+      for (size_t i = t; i < n; i += T) fn(i);
+    });
+  for (size_t i = 0; i < n; i += T) fn(i);
+  for (auto& th : ts) th.join();
 }
 
 }  // namespace
@@ -101,10 +186,27 @@ struct atls_stream_batch {
   bool keys_dirty = false;
   std::vector<Conn> conns;
   Pinned in, wire, pt;
+  size_t in_len = 0;  // bytes of queued writes in `in`
   std::vector<atls_rec> recs;
   std::vector<atls_open_result> res;
+  int threads = 1;
   std::mutex mu;
+  // env ATLS_SB_PROFILE=1: seconds per phase, printed to stderr by atls_sb_destroy
+  bool profile = std::getenv("ATLS_SB_PROFILE") != nullptr;
+  double t_write = 0, t_seal = 0, t_send = 0, t_recv = 0, t_poll = 0, t_gather = 0, t_open = 0, t_hand = 0;
 };
+
+namespace {
+struct Stopwatch {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  double lap() {
+    const auto n = std::chrono::steady_clock::now();
+    const double d = std::chrono::duration<double>(n - t).count();
+    t = n;
+    return d;
+  }
+};
+}  // namespace
 
 namespace {
 
@@ -128,6 +230,112 @@ int key_check(const atls_key& k) {
   return ATLS_INSUFFICIENT_SECURITY;
 }
 
+// The connection's error becomes visible to its readers (after the records opened before it).
+void publish_err(Conn& c) {
+  std::lock_guard<std::mutex> lk(c.inbox->mu);
+  if (c.err && !c.inbox->err) c.inbox->err = c.err;
+}
+
+long open_pending_locked(atls_stream_batch* sb) {
+  const size_t nc = sb->conns.size();
+  std::vector<size_t> wbase(nc + 1, 0), rbase(nc + 1, 0);
+  for (size_t i = 0; i < nc; i++) {
+    const Conn& c = sb->conns[i];
+    const bool any = !c.err && !c.offs.empty();
+    wbase[i + 1] = wbase[i] + (any ? c.rx_done : 0);
+    rbase[i + 1] = rbase[i] + (any ? c.offs.size() : 0);
+  }
+  const size_t n = rbase[nc], wire_bytes = wbase[nc];
+  if (n == 0) return 0;
+  if (n > 0xffffffffu) return -ATLS_ILLEGAL_PARAMETER;
+  int rc = install_keys(sb);
+  if (rc) return -rc;
+  // plaintexts packed back to back (the engine copies a gapless output range back in one piece)
+  if (!sb->wire.reserve(wire_bytes + 16) || !sb->pt.reserve(wire_bytes + 16)) return -ATLS_INTERNAL_ERROR;
+  std::vector<size_t> pbase(nc + 1, 0);
+  for (size_t i = 0; i < nc; i++) {
+    size_t ptb = 0;
+    const Conn& c = sb->conns[i];
+    if (rbase[i + 1] != rbase[i])
+      for (uint32_t o : c.offs) ptb += (((size_t)c.rx[o + 3] << 8) | c.rx[o + 4]) - 16;
+    pbase[i + 1] = pbase[i] + ptb;
+  }
+  sb->recs.assign(n, atls_rec{});
+  sb->res.assign(n, atls_open_result{});
+  Stopwatch sw;
+  parallel(sb->threads, nc, [&](size_t ci) {  // gather each connection's whole records, describe them
+    Conn& c = sb->conns[ci];
+    if (rbase[ci + 1] == rbase[ci]) return;
+    std::memcpy(sb->wire.p + wbase[ci], c.rx.data(), c.rx_done);
+    size_t po = pbase[ci];
+    for (size_t j = 0; j < c.offs.size(); j++) {
+      const uint8_t* h = c.rx.data() + c.offs[j];
+      atls_rec& d = sb->recs[rbase[ci] + j];
+      d.in_off = wbase[ci] + c.offs[j];
+      d.out_off = po;
+      po += (((uint32_t)h[3] << 8) | h[4]) - 16;
+      d.seq = c.rseq + j;
+      d.len = (((uint32_t)h[3] << 8) | h[4]) - 16;
+      d.key_slot = c.rslot;
+      d.mode = ATLS_MODE_WIRE;
+    }
+  });
+  sb->t_gather += sw.lap();
+  rc = atls_open_batch(sb->e, sb->recs.data(), (uint32_t)n, sb->wire.p, nullptr, nullptr, sb->pt.p, sb->res.data(), 0);
+  if (rc) return -rc;
+  sb->t_open += sw.lap();
+  parallel(sb->threads, nc, [&](size_t ci) {  // hand each connection its plaintexts, keep its partial tail
+    Conn& c = sb->conns[ci];
+    if (rbase[ci + 1] == rbase[ci]) return;
+    std::vector<Record> got;
+    got.reserve(c.offs.size());
+    for (size_t j = 0; j < c.offs.size(); j++) {
+      const atls_open_result& r = sb->res[rbase[ci] + j];
+      if (r.status) {  // a failed record ends the connection
+        c.err = r.status;
+        break;
+      }
+      const uint8_t* p = sb->pt.p + sb->recs[rbase[ci] + j].out_off;
+      got.push_back(Record{r.content_type, std::vector<uint8_t>(p, p + r.content_len)});
+    }
+    c.rseq += c.offs.size();
+    std::memmove(c.rx.data(), c.rx.data() + c.rx_done, c.rx_len - c.rx_done);
+    c.rx_len -= c.rx_done;
+    c.rx_done = 0;
+    c.offs.clear();
+    {
+      std::lock_guard<std::mutex> lk(c.inbox->mu);
+      for (Record& r : got) c.inbox->q.push_back(std::move(r));
+      if (c.err && !c.inbox->err) c.inbox->err = c.err;
+    }
+  });
+  sb->t_hand += sw.lap();
+  return (long)n;
+}
+
+// One record of the connection's inbox into buf: ATLS_OK, kUnexpectedMessage for a record that is not
+// application data (dropped, stream.rs:112-116), ATLS_ILLEGAL_PARAMETER when it does not fit (kept), the
+// connection's error once its inbox is empty, or -1 when nothing is there yet.
+int pop_inbox(Inbox& in, uint8_t* buf, size_t cap, size_t* out_len) {
+  std::lock_guard<std::mutex> lk(in.mu);
+  if (in.q.empty()) return in.err ? in.err : -1;
+  Record& r = in.q.front();
+  if (r.type != 23) {
+    in.q.pop_front();
+    return kUnexpectedMessage;
+  }
+  if (r.data.size() > cap) return ATLS_ILLEGAL_PARAMETER;
+  if (!r.data.empty()) std::memcpy(buf, r.data.data(), r.data.size());
+  *out_len = r.data.size();
+  in.q.pop_front();
+  return ATLS_OK;
+}
+
+Inbox* inbox_of(atls_stream_batch* sb, int conn) {
+  std::lock_guard<std::mutex> lk(sb->mu);
+  return valid_conn_locked(sb, conn) ? sb->conns[(size_t)conn].inbox.get() : nullptr;
+}
+
 }  // namespace
 
 extern "C" {
@@ -139,7 +347,20 @@ atls_stream_batch* atls_sb_create(atls_engine* e) {
   return sb;
 }
 
-void atls_sb_destroy(atls_stream_batch* sb) { delete sb; }
+void atls_sb_destroy(atls_stream_batch* sb) {
+  if (sb && sb->profile)
+    std::fprintf(stderr,
+                 "atls_sb profile (s): write %.4f seal %.4f send %.4f recv %.4f poll %.4f gather %.4f open %.4f hand %.4f\n",
+                 sb->t_write, sb->t_seal, sb->t_send, sb->t_recv, sb->t_poll, sb->t_gather, sb->t_open, sb->t_hand);
+  delete sb;
+}
+
+int atls_sb_set_threads(atls_stream_batch* sb, int threads) {
+  if (!sb || threads < 1 || threads > kMaxThreads) return ATLS_ILLEGAL_PARAMETER;
+  std::lock_guard<std::mutex> lk(sb->mu);
+  sb->threads = threads;
+  return ATLS_OK;
+}
 
 int atls_sb_add_connection(atls_stream_batch* sb, int fd, const atls_key* write_key, const atls_key* read_key) {
   if (!sb || !write_key || !read_key) return -ATLS_ILLEGAL_PARAMETER;
@@ -164,59 +385,70 @@ int atls_sb_write(atls_stream_batch* sb, int conn, uint8_t content_type, const u
   if (!valid_conn_locked(sb, conn)) return ATLS_ILLEGAL_PARAMETER;
   Conn& c = sb->conns[(size_t)conn];
   if (c.err) return c.err;
-  if (len == 0) c.out.push_back(Record{content_type, {}});
-  for (size_t off = 0; off < len; off += kMaxFragment) {
-    const size_t k = std::min(kMaxFragment, len - off);
-    c.out.push_back(Record{content_type, std::vector<uint8_t>(data + off, data + off + k)});
-  }
+  Stopwatch sw;
+  struct Add {
+    atls_stream_batch* sb;
+    Stopwatch& w;
+    ~Add() { sb->t_write += w.lap(); }
+  } add{sb, sw};
+  if (!sb->in.reserve(sb->in_len + len + 16, sb->in_len)) return ATLS_INTERNAL_ERROR;
+  if (len) std::memcpy(sb->in.p + sb->in_len, data, len);  // the only copy of the write on the host
+  if (len == 0) c.out.push_back(Queued{sb->in_len, 0, content_type});
+  for (size_t off = 0; off < len; off += kMaxFragment)
+    c.out.push_back(Queued{sb->in_len + off, (uint32_t)std::min(kMaxFragment, len - off), content_type});
+  sb->in_len += len;
   return ATLS_OK;
 }
 
 long atls_sb_flush(atls_stream_batch* sb) {
   if (!sb) return -ATLS_INTERNAL_ERROR;
   std::lock_guard<std::mutex> lk(sb->mu);
-  size_t n = 0, in_bytes = 0, wire_bytes = 0;
-  for (const Conn& c : sb->conns)
-    for (const Record& r : c.out) {
-      n++;
-      in_bytes += r.data.size();
-      wire_bytes += r.data.size() + 22;  // header 5, inner type 1, tag 16
-    }
+  const size_t nc = sb->conns.size();
+  std::vector<size_t> wbase(nc + 1, 0), rbase(nc + 1, 0);
+  for (size_t i = 0; i < nc; i++) {
+    size_t bytes = 0;
+    for (const Queued& r : sb->conns[i].out) bytes += r.len + 22;  // header 5, inner type 1, tag 16
+    wbase[i + 1] = wbase[i] + bytes;
+    rbase[i + 1] = rbase[i] + sb->conns[i].out.size();
+  }
+  const size_t n = rbase[nc];
   if (n == 0) return 0;
   if (n > 0xffffffffu) return -ATLS_ILLEGAL_PARAMETER;
   int rc = install_keys(sb);
   if (rc) return -rc;
-  if (!sb->in.reserve(in_bytes + 16) || !sb->wire.reserve(wire_bytes + 16)) return -ATLS_INTERNAL_ERROR;
+  if (!sb->wire.reserve(wbase[nc] + 16)) return -ATLS_INTERNAL_ERROR;
   sb->recs.assign(n, atls_rec{});
-  size_t i = 0, io = 0, wo = 0;
-  for (Conn& c : sb->conns) {
+  for (size_t ci = 0; ci < nc; ci++) {  // each connection's records back to back on its wire slice
+    const Conn& c = sb->conns[ci];
+    size_t wo = wbase[ci];
     uint64_t seq = c.wseq;
-    for (const Record& r : c.out) {
-      if (!r.data.empty()) std::memcpy(sb->in.p + io, r.data.data(), r.data.size());
-      atls_rec& d = sb->recs[i++];
-      d.in_off = io;
+    for (size_t j = 0; j < c.out.size(); j++) {
+      const Queued& r = c.out[j];
+      atls_rec& d = sb->recs[rbase[ci] + j];
+      d.in_off = r.in_off;
       d.out_off = wo;
       d.seq = seq++;
-      d.len = (uint32_t)r.data.size();
+      d.len = r.len;
       d.key_slot = c.wslot;
       d.content_type = r.type;
       d.mode = ATLS_MODE_WIRE;
-      io += r.data.size();
-      wo += r.data.size() + 22;
+      wo += r.len + 22;
     }
   }
+  Stopwatch sw;
   rc = atls_seal_batch(sb->e, sb->recs.data(), (uint32_t)n, sb->in.p, nullptr, sb->wire.p, nullptr, 0);
   if (rc) return -rc;
-  wo = 0;
-  for (Conn& c : sb->conns) {
-    if (c.out.empty()) continue;
-    size_t bytes = 0;
-    for (const Record& r : c.out) bytes += r.data.size() + 22;
+  sb->t_seal += sw.lap();
+  sb->in_len = 0;
+  parallel(sb->threads, nc, [&](size_t ci) {
+    Conn& c = sb->conns[ci];
+    if (c.out.empty()) return;
     c.wseq += c.out.size();
     c.out.clear();
-    if (!c.err && !send_all(c.fd, sb->wire.p + wo, bytes)) c.err = kBrokenPipe;
-    wo += bytes;
-  }
+    if (!c.err && !send_all(c.fd, sb->wire.p + wbase[ci], wbase[ci + 1] - wbase[ci])) c.err = kBrokenPipe;
+  });
+  sb->t_send += sw.lap();
+  for (Conn& c : sb->conns) publish_err(c);
   return (long)n;
 }
 
@@ -225,8 +457,10 @@ int atls_sb_feed(atls_stream_batch* sb, int conn, const uint8_t* data, size_t le
   std::lock_guard<std::mutex> lk(sb->mu);
   if (!valid_conn_locked(sb, conn)) return ATLS_ILLEGAL_PARAMETER;
   Conn& c = sb->conns[(size_t)conn];
-  c.rx.insert(c.rx.end(), data, data + len);
-  if (!c.err) split(c);
+  if (c.rx_len + len > kRxMax) return ATLS_ILLEGAL_PARAMETER;
+  if (len) append_rx(c, data, len);
+  scan(c);
+  publish_err(c);
   return c.err;
 }
 
@@ -245,110 +479,80 @@ long atls_sb_recv(atls_stream_batch* sb, int conn, size_t max_bytes) {
     k = recv(fd, buf.data(), max_bytes, 0);
   } while (k < 0 && errno == EINTR);
   if (k < 0) return -kBrokenPipe;
-  if (k == 0) return 0;
+  if (k == 0) {
+    std::lock_guard<std::mutex> lk(sb->mu);
+    sb->conns[(size_t)conn].eof = true;
+    return 0;
+  }
   const int rc = atls_sb_feed(sb, conn, buf.data(), (size_t)k);
   return rc ? -rc : (long)k;
+}
+
+long atls_sb_recv_all(atls_stream_batch* sb, int timeout_ms) {
+  if (!sb) return -ATLS_INTERNAL_ERROR;
+  std::lock_guard<std::mutex> lk(sb->mu);
+  const size_t nc = sb->conns.size();
+  Stopwatch sw;
+  for (int round = 0; round < 2; round++) {
+    std::atomic<size_t> total{0};
+    parallel(sb->threads, nc, [&](size_t ci) { total += drain_socket(sb->conns[ci]); });
+    for (Conn& c : sb->conns) publish_err(c);
+    sb->t_recv += sw.lap();
+    if (total.load() || timeout_ms <= 0 || round) return (long)total.load();
+    std::vector<pollfd> fds;  // nothing arrived: wait for any open connection, once
+    for (const Conn& c : sb->conns)
+      if (!c.err && !c.eof && c.rx_len < kRxMax) fds.push_back(pollfd{c.fd, POLLIN, 0});
+    const int pr = fds.empty() ? 0 : poll(fds.data(), fds.size(), timeout_ms);
+    sb->t_poll += sw.lap();
+    if (pr <= 0) return 0;
+  }
+  return 0;
 }
 
 long atls_sb_open_pending(atls_stream_batch* sb) {
   if (!sb) return -ATLS_INTERNAL_ERROR;
   std::lock_guard<std::mutex> lk(sb->mu);
-  size_t n = 0, wire_bytes = 0, pt_bytes = 0;
-  for (const Conn& c : sb->conns) {
-    if (c.err || c.offs.empty()) continue;
-    n += c.offs.size();
-    wire_bytes += c.wire.size();
-    pt_bytes += c.wire.size();  // >= the ciphertext bytes
-  }
-  if (n == 0) return 0;
-  int rc = install_keys(sb);
-  if (rc) return -rc;
-  if (!sb->wire.reserve(wire_bytes + 16) || !sb->pt.reserve(pt_bytes + 16)) return -ATLS_INTERNAL_ERROR;
-  sb->recs.assign(n, atls_rec{});
-  sb->res.assign(n, atls_open_result{});
-  size_t i = 0, wo = 0, po = 0;
-  for (Conn& c : sb->conns) {
-    if (c.err || c.offs.empty()) continue;
-    std::memcpy(sb->wire.p + wo, c.wire.data(), c.wire.size());
-    for (size_t j = 0; j < c.offs.size(); j++) {
-      const uint8_t* h = c.wire.data() + c.offs[j];
-      const uint32_t ct = (((uint32_t)h[3] << 8) | h[4]) - 16;
-      atls_rec& d = sb->recs[i++];
-      d.in_off = wo + c.offs[j];
-      d.out_off = po;
-      d.seq = c.rseq + j;
-      d.len = ct;
-      d.key_slot = c.rslot;
-      d.mode = ATLS_MODE_WIRE;
-      po += ct;
-    }
-    wo += c.wire.size();
-  }
-  rc = atls_open_batch(sb->e, sb->recs.data(), (uint32_t)n, sb->wire.p, nullptr, nullptr, sb->pt.p, sb->res.data(), 0);
-  if (rc) return -rc;
-  i = 0;
-  for (Conn& c : sb->conns) {
-    if (c.err || c.offs.empty()) continue;
-    for (size_t j = 0; j < c.offs.size(); j++, i++) {
-      if (c.err) continue;  // a failed record ends the connection
-      const atls_open_result& r = sb->res[i];
-      if (r.status) {
-        c.err = r.status;
-        continue;
-      }
-      const uint8_t* p = sb->pt.p + sb->recs[i].out_off;
-      c.inbox.push_back(Record{r.content_type, std::vector<uint8_t>(p, p + r.content_len)});
-    }
-    c.rseq += c.offs.size();
-    c.wire.clear();
-    c.offs.clear();
-  }
-  return (long)n;
+  return open_pending_locked(sb);
+}
+
+int atls_sb_read_ready(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size_t* out_len) {
+  if (!sb || !out_len || (cap && !buf)) return ATLS_ILLEGAL_PARAMETER;
+  Inbox* in = inbox_of(sb, conn);
+  if (!in) return ATLS_ILLEGAL_PARAMETER;
+  // the inbox outlives a conns growth (it is owned through a pointer), so it is read without sb->mu
+  const int rc = pop_inbox(*in, buf, cap, out_len);
+  return rc < 0 ? ATLS_WOULD_BLOCK : rc;
 }
 
 int atls_sb_read(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size_t* out_len) {
   if (!sb || !out_len || (cap && !buf)) return ATLS_ILLEGAL_PARAMETER;
   for (;;) {
-    bool pending;
+    const int rc = atls_sb_read_ready(sb, conn, buf, cap, out_len);
+    if (rc != ATLS_WOULD_BLOCK) return rc;
+    bool pending, eof;
     {
       std::lock_guard<std::mutex> lk(sb->mu);
-      if (!valid_conn_locked(sb, conn)) return ATLS_ILLEGAL_PARAMETER;
       Conn& c = sb->conns[(size_t)conn];
-      if (!c.inbox.empty()) {
-        Record& r = c.inbox.front();
-        if (r.type != 23) {  // stream.rs:112-116
-          c.inbox.pop_front();
-          return kUnexpectedMessage;
-        }
-        if (r.data.size() > cap) return ATLS_ILLEGAL_PARAMETER;  // kept for a larger buffer
-        if (!r.data.empty()) std::memcpy(buf, r.data.data(), r.data.size());
-        *out_len = r.data.size();
-        c.inbox.pop_front();
-        return ATLS_OK;
+      if (c.err) {
+        publish_err(c);
+        continue;  // the error reaches the reader after the records before it
       }
-      if (c.err) return c.err;
       pending = !c.offs.empty();
+      eof = c.eof;
     }
     if (pending) {
       const long k = atls_sb_open_pending(sb);
       if (k < 0) return (int)-k;
+    } else if (eof) {
+      return kBrokenPipe;
     } else {
       const long k = atls_sb_recv(sb, conn, size_t(1) << 20);
       if (k == 0) return kBrokenPipe;
       if (k < 0) return (int)-k;
       // take whatever else has arrived before opening, so one batch covers it all
-      int fd;
-      {
-        std::lock_guard<std::mutex> lk(sb->mu);
-        fd = sb->conns[(size_t)conn].fd;
-      }
-      thread_local std::vector<uint8_t> more(size_t(1) << 20);
-      for (;;) {
-        const ssize_t m = recv(fd, more.data(), more.size(), MSG_DONTWAIT);
-        if (m <= 0) break;  // EAGAIN, EOF (seen by the next blocking read) or an error
-        const int rc = atls_sb_feed(sb, conn, more.data(), (size_t)m);
-        if (rc) return rc;
-      }
+      std::lock_guard<std::mutex> lk(sb->mu);
+      drain_socket(sb->conns[(size_t)conn]);
+      publish_err(sb->conns[(size_t)conn]);
     }
   }
 }

@@ -77,6 +77,7 @@ def parse():
     p.add_argument("--sustain-s", type=float, default=5.0,
                    help="after the timed steps, seal the headline batch back to back for this long (every rank) "
                         "and report the sustained rate (clocks under continuous load); 0 = skip")
+    p.add_argument("--c1-threads", type=int, default=8, help="C1 at scale: worker threads per stream batch")
     p.add_argument("--dry-run-cap", type=int, default=64,
                    help="--dry-run: content bytes per record of the whole-batch exchange rehearsal")
     p.add_argument("--dry-run", action="store_true",
@@ -241,6 +242,24 @@ def run_c1(args):
               "data": "synthetic 1 MiB body, RFC 8448 server traffic secret",
               "config": {"workload": C1, "records_per_body": c1.N_REC, "record_content": c1.CONTENT,
                          "suite": "TLS_AES_128_GCM_SHA256", "path": "anothertls_amd.stream.StreamBatch (WIRE mode)"}}
+    # C1 at scale: the native batched socket path (tools/c1_loopback_native, atls_sb_* with
+    # worker threads) over 64 and 256 connections, every byte checked by the tool
+    exe = os.path.join(ROOT, "tools", "c1_loopback_native")
+    if os.path.exists(exe):
+        import subprocess
+
+        scale = []
+        for conns, reps in ((64, 8), (256, 2)):
+            for threads in (1, args.c1_threads):
+                out = subprocess.run([exe, str(reps), str(conns), str(threads)], capture_output=True, text=True,
+                                     timeout=300)
+                line = json.loads(out.stdout.strip().splitlines()[-1]) if out.returncode == 0 and out.stdout.strip() \
+                    else {"error": out.stderr[-300:]}
+                line.pop("config", None)
+                scale.append(line)
+        result["at_scale"] = {"runs": scale, "unit": "MB/s of response body, seal -> 127.0.0.1 TCP -> open, every byte checked",
+                              "path": "native atls_stream_batch, one WIRE seal batch per flush and one open batch per "
+                                      "receive round, T worker threads (atls_sb_set_threads)"}
     if not args.no_cpu_baseline:
         t = c1_cpu_reference(body, 1)
         result["cpu_baseline"] = {"value": round(len(body) / t / 1e6, 3), "unit": "MB/s", "cores": 1,

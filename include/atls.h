@@ -85,11 +85,13 @@ enum {
                                  as ATLS_ILLEGAL_PARAMETER by that atls_engine_sync, or by any
                                  later synchronous call on the engine (the error word is sticky
                                  until a synchronous call reads it). */
-  ATLS_FLAG_LAZY_JOIN = 8u    /* with NO_SYNC and DEVICE_PTRS: a mixed-suite batch's ChaCha20-Poly1305
-                                 kernel (second stream) is not joined back into the engine stream
-                                 at the end of the batch; the next batch's plan and AES-GCM kernel
-                                 may start beside it. The engine stream covers it again after
-                                 atls_engine_join / atls_engine_sync or a batch without this flag.
+  ATLS_FLAG_LAZY_JOIN = 8u    /* honoured only with NO_SYNC, DEVICE_PTRS, DEVICE_RECS and a caller tags
+                                 array (the side kernel then reads no engine-owned buffer); otherwise the
+                                 batch joins as usual. A mixed-suite batch's ChaCha20-Poly1305 kernel
+                                 (second stream) is not joined back into the engine stream at the end of
+                                 the batch; the next batch's plan and AES-GCM kernel may start beside it.
+                                 The engine stream covers it again after atls_engine_join /
+                                 atls_engine_sync, a batch without this flag, or a key-table update.
                                  Batches of one engine stay ordered per record kernel. */
 };
 
@@ -149,8 +151,12 @@ int atls_open(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t*
 atls_engine* atls_engine_create(int device); /* NULL if the device is unusable */
 void atls_engine_destroy(atls_engine* e);
 /* Wait until everything enqueued on the engine has finished; reports a descriptor a NO_SYNC batch refused.
- * Waits on a completion flag a one-lane kernel writes into mapped memory (env ATLS_SYNC_FLAG=0: a stream
- * synchronisation instead). */
+ * Waits on a completion flag a one-lane kernel writes into mapped memory after a system-scope release (which
+ * also writes back the L2 lines the batch's kernels left, host-mapped outputs of DEVICE_PTRS batches
+ * included), spinning for at most 100 us and then blocking in a stream synchronisation (env
+ * ATLS_SYNC_FLAG=0: a stream synchronisation only). Synchronous batches return the same way; batches that
+ * copy into host memory, or read and write page-locked host buffers in place (ATLS_ZERO_COPY), synchronise
+ * the stream. */
 int atls_engine_sync(atls_engine* e);
 /* HIP stream the engine launches on (hipStream_t as void*), for callers that time or order work.
  * Work of ATLS_FLAG_LAZY_JOIN batches is on it only after atls_engine_join. */
@@ -160,10 +166,14 @@ void* atls_engine_stream(atls_engine* e);
 int atls_engine_join(atls_engine* e);
 
 /* Install n key slots (host array). Runs the device key-setup kernel: AES round keys, H = E_K(0),
- * H^1..H^64 and the GHASH table seeds; ChaCha keys are used as given. Replaces previous slots. */
+ * H^1..H^64 and the GHASH table seeds; ChaCha keys are used as given. Replaces previous slots.
+ * Up to 4 keys travel in the kernel's launch arguments and the call returns without waiting for the
+ * kernel (every later batch of the engine is ordered after it); a fault of that kernel is then reported
+ * by the next synchronous call or atls_engine_sync. More keys are staged by a copy and waited for. */
 int atls_set_keys(atls_engine* e, const atls_key* keys, uint32_t n);
 /* Install n key slots at [first, first + n) without touching the others (connections come and go);
- * first <= the current slot count (slots stay contiguous; the table grows as needed). */
+ * first <= the current slot count (slots stay contiguous; the table grows as needed). Waits as
+ * atls_set_keys does. */
 int atls_update_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t n);
 
 /* Seal / open n records. */
@@ -232,6 +242,12 @@ atls_multi* atls_multi_create(const int* devices, int n_devices); /* NULL if a d
 void atls_multi_destroy(atls_multi* m);
 int atls_multi_devices(const atls_multi* m);
 int atls_multi_uses_rccl(const atls_multi* m); /* 1: RCCL transport, 0: device copies / single device */
+/* The RCCL actually loaded (ncclGetVersion, e.g. 22606 = 2.26.6; 0 without RCCL) and the largest
+ * point-to-point message the multi engine sends (ranges go in pieces of at most this many bytes;
+ * env ATLS_MULTI_CHUNK_MB, default 1 GiB: RCCL 2.26.6 corrupts self messages past 2^30 bytes).
+ * The version and the cap are also printed to stderr once per process. */
+int atls_multi_rccl_version(const atls_multi* m);
+size_t atls_multi_max_message(const atls_multi* m);
 int atls_multi_set_keys(atls_multi* m, const atls_key* keys, uint32_t n);
 int atls_multi_seal_batch(atls_multi* m, const atls_rec* recs, uint32_t n, const void* in, const void* aux, void* out,
                           uint8_t* tags, uint32_t flags);
@@ -244,27 +260,40 @@ void atls_partition(const atls_rec* recs, uint32_t n, int open, uint32_t parts, 
 
 /* ---- Batched record streams (TlsStream::tls_write / tls_read, net/stream.rs:32-150) -------
  * Many connections over one engine: atls_sb_write queues a connection's records (fragmented at
- * 2^14 bytes, RFC 8446 §5.1), atls_sb_flush seals the queued records of every connection in one
- * ATLS_MODE_WIRE batch and send()s each connection's wire bytes; received bytes (atls_sb_recv
- * from the socket, or atls_sb_feed) are split into whole records (Record::from_raw,
- * record.rs:81-102), atls_sb_open_pending opens every connection's complete records in one
- * batch, atls_sb_read returns the next application-data record of a connection (blocking:
- * receives and opens as needed; UnexpectedMessage (10) for other content types, stream.rs:112-116;
- * BrokenPipe (254) at end of stream). Each connection has a write key and a read key with their
- * own sequence numbers (key_schedule.rs:51-64); a record that fails ends its connection with
- * the record layer's error (50 / 51), which later calls return. Functions returning long give
- * a count (>= 0) or minus a TlsError code. One batch per thread at a time. */
+ * 2^14 bytes, RFC 8446 §5.1; the data is copied once, into the batch's page-locked input), atls_sb_flush
+ * seals the queued records of every connection in one ATLS_MODE_WIRE batch and send()s each connection's
+ * wire bytes; received bytes (atls_sb_recv / atls_sb_recv_all from the sockets, or atls_sb_feed) are
+ * split into whole records (Record::from_raw, record.rs:81-102), atls_sb_open_pending opens every
+ * connection's complete records in one batch, atls_sb_read returns the next application-data record of a
+ * connection (blocking: receives and opens as needed; UnexpectedMessage (10) for other content types,
+ * stream.rs:112-116; BrokenPipe (254) at end of stream). Each connection has a write key and a read key
+ * with their own sequence numbers (key_schedule.rs:51-64); a record that fails ends its connection with
+ * the record layer's error (50 / 51), which its reader gets after the records before it. Functions
+ * returning long give a count (>= 0) or minus a TlsError code.
+ * Threads: atls_sb_set_threads(sb, T) (1..64, default 1) spreads flush's sends, atls_sb_recv_all's
+ * receives and open_pending's gather / hand-over over T threads (by connection). Calls on one batch
+ * are serialised, except atls_sb_read_ready (and the copy-out of atls_sb_read), which take only the
+ * connection's own lock: readers of different connections copy out in parallel. */
 typedef struct atls_stream_batch atls_stream_batch;
+enum { ATLS_WOULD_BLOCK = 253 }; /* atls_sb_read_ready: no opened record yet (not a TlsError) */
 atls_stream_batch* atls_sb_create(atls_engine* e);
 void atls_sb_destroy(atls_stream_batch* sb);
+int atls_sb_set_threads(atls_stream_batch* sb, int threads);
 /* fd: a connected stream socket; returns the connection id (>= 0) or -code. */
 int atls_sb_add_connection(atls_stream_batch* sb, int fd, const atls_key* write_key, const atls_key* read_key);
 int atls_sb_write(atls_stream_batch* sb, int conn, uint8_t content_type, const uint8_t* data, size_t len);
 long atls_sb_flush(atls_stream_batch* sb);                       /* records sealed and sent */
 int atls_sb_feed(atls_stream_batch* sb, int conn, const uint8_t* data, size_t len);
 long atls_sb_recv(atls_stream_batch* sb, int conn, size_t max_bytes); /* bytes read; 0 at EOF */
+/* Every connection's socket drained without blocking (T threads), straight into its receive buffer;
+ * when nothing at all arrived, waits up to timeout_ms for any connection and drains once more. Returns
+ * the bytes received. */
+long atls_sb_recv_all(atls_stream_batch* sb, int timeout_ms);
 long atls_sb_open_pending(atls_stream_batch* sb);                /* records opened */
 int atls_sb_read(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size_t* out_len);
+/* As atls_sb_read without receiving or opening: an opened record, the connection's error once its
+ * opened records are read, or ATLS_WOULD_BLOCK. */
+int atls_sb_read_ready(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size_t* out_len);
 
 /* Diagnostic (no reference counterpart): the shader clock the device runs at under the current load, for
  * rooflines counted in cycles. Enqueues wgs (1..1024) one-wave workgroups on `stream`

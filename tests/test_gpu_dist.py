@@ -252,3 +252,49 @@ def test_multi_engine_refuses_before_queueing(rccl_self, monkeypatch):
     m.seal_batch(b["recs"], d_in, d_aux, d_out, d_tags, flags=atls.FLAG_DEVICE_PTRS)  # no stale error
     assert np.array_equal(d_out.cpu().numpy(), ref_out) and np.array_equal(d_tags.cpu().numpy(), ref_tags)
     m.close()
+
+
+@pytest.mark.parametrize("per_part", [65535, 65536, 65537], ids=["under", "at", "over"])
+def test_rccl_message_cap_boundary(per_part, monkeypatch):
+    """The RCCL message cap at its real size: two parts in RCCL-self mode, part 1's range of
+    `per_part` 16 KiB records -- 2^30 - 16 KiB, exactly 2^30 and 2^30 + 16 KiB of input (one, one and two
+    messages), and 16,400-B output slots (just over 2^30 each time: two messages) -- sealed and opened,
+    equal to one engine byte for byte; the loaded RCCL's version and the 1 GiB cap are reported."""
+    monkeypatch.setenv("ATLS_MULTI_RCCL_SELF", "1")
+    monkeypatch.delenv("ATLS_MULTI_CHUNK_MB", raising=False)
+    n = 2 * per_part
+    b = workload.config_batch("c2_aes128gcm_64Ki_x_16KiB", n=n, n_keys=64)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(7)
+    d_in = torch.randint(0, 256, (b["in_bytes"] + 16,), dtype=torch.uint8, device=dev, generator=g)
+    d_aux = torch.zeros(16, dtype=torch.uint8, device=dev)
+    first = atls.partition(b["recs"], 2)
+    assert int(first[1]) == per_part
+    e = atls.Engine(0)
+    e.set_keys(b["keys"])
+    ref_out = torch.zeros(b["out_bytes"] + 16, dtype=torch.uint8, device=dev)
+    ref_tags = torch.zeros(16 * n, dtype=torch.uint8, device=dev)
+    e.seal_batch(b["recs"], d_in, d_aux, ref_out, ref_tags, flags=atls.FLAG_DEVICE_PTRS)
+    e.close()
+    m = atls.MultiEngine([0, 0])
+    try:
+        assert m.uses_rccl and m.rccl_version >= 22600 and m.max_message == 1 << 30
+        m.set_keys(b["keys"])
+        out = torch.zeros_like(ref_out)
+        tags = torch.zeros_like(ref_tags)
+        m.seal_batch(b["recs"], d_in, d_aux, out, tags, flags=atls.FLAG_DEVICE_PTRS)
+        torch.cuda.synchronize()
+        assert torch.equal(tags, ref_tags) and torch.equal(out, ref_out)
+        orecs = b["recs"].copy()
+        orecs["in_off"], orecs["len"] = b["recs"]["out_off"], b["recs"]["len"] + 1
+        pt = torch.zeros_like(out)
+        res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
+        m.open_batch(orecs, out, d_aux, tags, pt, res, flags=atls.FLAG_DEVICE_PTRS)
+        torch.cuda.synchronize()
+        r = res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
+        assert (r["status"] == 0).all() and (r["content_len"] == 16384).all()
+        assert torch.equal(pt[: n * 16400].view(n, 16400)[:, :16384], d_in[: n * 16384].view(n, 16384))
+    finally:
+        m.close()
+        del d_in, ref_out
+        torch.cuda.empty_cache()

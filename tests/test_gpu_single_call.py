@@ -207,3 +207,30 @@ def test_chacha_four_wave_record_vs_oracle():
             assert c.decrypt(key, iv, ct, aad, tag) == pt
             with pytest.raises(atls.TlsError):
                 c.decrypt(key, iv, ct, aad, tag[:15] + bytes([tag[15] ^ 0x40]))
+
+
+@pytest.mark.parametrize("suite,klen", [(0x1301, 16), (0x1302, 32), (0x1303, 32)])
+def test_long_single_calls_vs_oracle(suite, klen):
+    """Single calls far past the argument block: AES-GCM records around the counter cache's
+    limit (16,384 slots = 262,144 B of slots: past it gcm_record runs without the cache) and just past the
+    1 MiB read-in-place limit (the record is copied into device memory first), 12- and 16-byte IVs, AADs of
+    0 / 5 / 40 bytes; ChaCha20-Poly1305 across the same 1 MiB limit. Seal, open and a tampered tag against
+    the oracle (crypto/aes/gcm.rs:42-162, crypto/chacha20/poly1305.rs:69-104)."""
+    rng = np.random.default_rng(klen * 101 + suite)
+    key = rng.integers(0, 256, klen, dtype=np.uint8).tobytes()
+    c = atls.CipherSuite(suite).get_cipher()
+    gcm = suite != 0x1303
+    lens = (262096, 262112, 262128, 262145, 1048560, 1048577) if gcm else (1048512, 1048576, 1048577)
+    for iv_len in ((12, 16) if gcm else (12,)):
+        for aad_len in (0, 5, 40):
+            for n in lens:
+                iv = rng.integers(0, 256, iv_len, dtype=np.uint8).tobytes()
+                aad = rng.integers(0, 256, aad_len, dtype=np.uint8).tobytes()
+                pt = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+                ct, tag = c.encrypt(key, iv, pt, aad)
+                rc, ect, etag = ora.cipher_encrypt(suite, key, iv, pt, aad)
+                assert rc == 0 and ct == ect and tag == etag, (iv_len, aad_len, n)
+                assert c.decrypt(key, iv, ct, aad, tag) == pt
+                with pytest.raises(atls.TlsError) as e:
+                    c.decrypt(key, iv, ct, aad, tag[:3] + bytes([tag[3] ^ 0x10]) + tag[4:])
+                assert e.value.code == 20

@@ -37,6 +37,12 @@ def atls():
     lib.atls_sb_flush.argtypes = [P]
     lib.atls_sb_feed.argtypes = [P, C.c_int, P, C.c_size_t]
     lib.atls_sb_read.argtypes = [P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.atls_sb_read_ready.argtypes = [P, C.c_int, P, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.atls_sb_set_threads.argtypes = [P, C.c_int]
+    lib.atls_sb_recv_all.restype = C.c_long
+    lib.atls_sb_recv_all.argtypes = [P, C.c_int]
+    lib.atls_sb_open_pending.restype = C.c_long
+    lib.atls_sb_open_pending.argtypes = [P]
     return a
 
 
@@ -125,12 +131,87 @@ def test_native_stream_batch(atls):
     e_c.close()
 
 
+def test_native_stream_batch_threads(atls):
+    """The multi-threaded socket path: 4 worker threads per batch. Flush sends every
+    connection's slice from the workers; connection 0's wire bytes are taken off its socket and compared with
+    the oracle's records, then fed back; the other connections arrive through atls_sb_recv_all (straight into
+    their receive buffers), atls_sb_open_pending (gather and hand-over on the workers) and atls_sb_read_ready
+    from several reader threads at once."""
+    import threading
+
+    lib = atls.library()
+    e_s, e_c = atls.Engine(0), atls.Engine(0)
+    s_sb, c_sb = lib.atls_sb_create(e_s._e), lib.atls_sb_create(e_c._e)
+    assert lib.atls_sb_set_threads(s_sb, 4) == 0 and lib.atls_sb_set_threads(c_sb, 4) == 0
+    assert lib.atls_sb_set_threads(c_sb, 0) == 47 and lib.atls_sb_set_threads(c_sb, 65) == 47
+    n = 12
+    pairs = [socket.socketpair() for _ in range(n)]
+    keys = [_keys(atls, i) for i in range(n)]
+    sconn = [lib.atls_sb_add_connection(s_sb, a.fileno(), w.ctypes.data, r.ctypes.data)
+             for (a, _), (w, r) in zip(pairs, keys)]
+    cconn = [lib.atls_sb_add_connection(c_sb, b.fileno(), r.ctypes.data, w.ctypes.data)
+             for (_, b), (w, r) in zip(pairs, keys)]
+    rng = np.random.default_rng(11)
+    sent = [[rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in rng.integers(0, 40000, 5)]
+            for _ in range(n)]
+    for rnd in range(2):  # two flushes: sequence numbers continue across them
+        for i in range(n):
+            for d in sent[i][rnd::2]:
+                assert lib.atls_sb_write(s_sb, sconn[i], 23, d, len(d)) == 0
+        assert lib.atls_sb_flush(s_sb) > 0
+    want, seq = b"", 0
+    w = keys[0][0][0]
+    for d in sent[0][0::2] + sent[0][1::2]:
+        for f in [d[j:j + 16384] for j in range(0, len(d), 16384)] or [b""]:
+            rc, rec = ora.record_seal(int(w["suite"]), bytes(w["key"][:int(w["key_len"])]), bytes(w["static_iv"]), seq, 23, f)
+            assert rc == 0
+            want += rec
+            seq += 1
+    raw = b""
+    while len(raw) < len(want):
+        raw += pairs[0][1].recv(1 << 20)
+    assert raw == want
+    assert lib.atls_sb_feed(c_sb, cconn[0], raw, len(raw)) == 0
+    expect = [b"".join(sent[i][0::2] + sent[i][1::2]) for i in range(n)]
+    got = [b""] * n
+    lock = threading.Lock()
+    for _ in range(200):
+        if all(len(got[i]) == len(expect[i]) for i in range(n)):
+            break
+        assert lib.atls_sb_recv_all(c_sb, 200) >= 0
+        assert lib.atls_sb_open_pending(c_sb) >= 0
+
+        def reader(t):
+            buf = (C.c_uint8 * 16384)()
+            ln = C.c_size_t(0)
+            for i in range(t, n, 3):
+                while (rc := lib.atls_sb_read_ready(c_sb, cconn[i], buf, 16384, C.byref(ln))) == 0:
+                    with lock:
+                        got[i] += bytes(buf[:ln.value])
+                assert rc == 253, rc  # ATLS_WOULD_BLOCK
+
+        ths = [threading.Thread(target=reader, args=(t,)) for t in range(3)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+    assert got == expect
+    for sb in (s_sb, c_sb):
+        lib.atls_sb_destroy(sb)
+    for a, b in pairs:
+        a.close()
+        b.close()
+    e_s.close()
+    e_c.close()
+
+
 @pytest.mark.timeout(120)
-def test_c1_native_loopback_tool(atls):
+@pytest.mark.parametrize("conns,threads", [(4, 1), (16, 4)])
+def test_c1_native_loopback_tool(atls, conns, threads):
     exe = os.path.join(ROOT, "tools", "c1_loopback_native")
     if not os.path.exists(exe):
         pytest.skip("tools/c1_loopback_native not built (tools/build_native.sh)")
-    out = subprocess.run([exe, "2", "4"], capture_output=True, text=True, timeout=100)
+    out = subprocess.run([exe, "2", str(conns), str(threads)], capture_output=True, text=True, timeout=100)
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
-    assert line["verified"] is True and line["gpu_MBps"] > 0
+    assert line["verified"] is True and line["gpu_MBps"] > 0 and line["threads"] == threads

@@ -5,9 +5,13 @@
 // connection's pending records together, and checks every byte. Keys: the RFC 8448 §3 server
 // handshake traffic secret through atls_derive_keys (Key::from_hkdf, key_schedule.rs:40-50).
 // Prints one JSON line: MB/s of body through seal -> socket -> open.
+// With threads > 1 (C1 at scale) both batches use that many worker threads
+// (atls_sb_set_threads): the server's flush sends from T threads; the client receives every connection
+// with atls_sb_recv_all, opens everything pending in one batch, and T reader threads take the opened
+// records of their connections (atls_sb_read_ready) and compare every byte.
 //
 // Built by __graft_entry__.build() with tools/build_native.sh (g++, linked to libatls.so).
-// Usage: tools/c1_loopback_native [reps=8] [conns=1]
+// Usage: tools/c1_loopback_native [reps=8] [conns=1] [threads=1]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
@@ -57,6 +61,7 @@ bool tcp_pair(int* server_fd, int* client_fd) {
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? std::atoi(argv[1]) : 8;
   const int conns = argc > 2 ? std::atoi(argv[2]) : 1;
+  const int threads = argc > 3 ? std::atoi(argv[3]) : 1;
   atls_engine* es = atls_engine_create(0);
   atls_engine* ec = atls_engine_create(0);
   if (!es || !ec) {
@@ -76,6 +81,7 @@ int main(int argc, char** argv) {
   }
   atls_stream_batch* ss = atls_sb_create(es);
   atls_stream_batch* cs = atls_sb_create(ec);
+  if (atls_sb_set_threads(ss, threads) || atls_sb_set_threads(cs, threads)) return 5;
   std::vector<int> sc(conns), cc(conns), fds;
   for (int i = 0; i < conns; i++) {
     int s, c;
@@ -95,15 +101,51 @@ int main(int argc, char** argv) {
         if (atls_sb_flush(ss) < 0) ok = false;
       }
     });
-    std::vector<uint8_t> buf(kContent);
-    for (int r = 0; r < n; r++)
-      for (int i = 0; i < conns; i++)
-        for (int k = 0; k < kRecords; k++) {
-          size_t got = 0;
-          if (atls_sb_read(cs, cc[i], buf.data(), buf.size(), &got) || got != kContent ||
-              std::memcmp(buf.data(), body.data() + k * kContent, kContent))
-            ok = false;
+    if (threads <= 1) {  // the reference's shape: one tls_read per record, in order
+      std::vector<uint8_t> buf(kContent);
+      for (int r = 0; r < n; r++)
+        for (int i = 0; i < conns; i++)
+          for (int k = 0; k < kRecords; k++) {
+            size_t got = 0;
+            if (atls_sb_read(cs, cc[i], buf.data(), buf.size(), &got) || got != kContent ||
+                std::memcmp(buf.data(), body.data() + k * kContent, kContent))
+              ok = false;
+          }
+    } else {  // receive everything pending, open it in one batch, read out on T threads
+      std::vector<long> left(conns, (long)n * kRecords);
+      long remaining = (long)n * kRecords * conns;
+      auto t_idle = std::chrono::steady_clock::now();
+      while (remaining > 0 && ok) {
+        const long got = atls_sb_recv_all(cs, 100);
+        if (got < 0 || atls_sb_open_pending(cs) < 0) {
+          ok = false;
+          break;
         }
+        std::atomic<long> taken{0};
+        std::vector<std::thread> rd;
+        for (int t = 0; t < threads; t++)
+          rd.emplace_back([&, t] {
+            std::vector<uint8_t> buf(kContent);
+            for (int i = t; i < conns; i += threads)
+              for (;;) {
+                size_t len = 0;
+                const int rc = atls_sb_read_ready(cs, cc[i], buf.data(), buf.size(), &len);
+                if (rc == ATLS_WOULD_BLOCK) break;
+                const long k = (long)n * kRecords - left[i];
+                if (rc || len != kContent || std::memcmp(buf.data(), body.data() + (k % kRecords) * kContent, kContent)) {
+                  ok = false;
+                  return;
+                }
+                left[i]--;
+                taken++;
+              }
+          });
+        for (auto& th : rd) th.join();
+        remaining -= taken.load();
+        if (got > 0 || taken.load() > 0) t_idle = std::chrono::steady_clock::now();
+        else if (std::chrono::steady_clock::now() - t_idle > std::chrono::seconds(20)) ok = false;  // stalled
+      }
+    }
     server.join();
   };
   run(1);  // warm-up: device buffers, code objects, pinned staging
@@ -112,8 +154,8 @@ int main(int argc, char** argv) {
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   std::printf("{\"config\": \"c1_server_https_loopback_1MiB\", \"impl\": \"native atls_stream_batch\", "
               "\"suite\": \"TLS_AES_128_GCM_SHA256\", \"records_per_body\": %d, \"conns\": %d, \"reps\": %d, "
-              "\"verified\": %s, \"gpu_MBps\": %.1f}\n",
-              kRecords, conns, reps, ok.load() ? "true" : "false", (double)reps * conns * kBody / dt / 1e6);
+              "\"threads\": %d, \"verified\": %s, \"gpu_MBps\": %.1f}\n",
+              kRecords, conns, reps, threads, ok.load() ? "true" : "false", (double)reps * conns * kBody / dt / 1e6);
   for (int fd : fds) close(fd);
   atls_sb_destroy(ss);
   atls_sb_destroy(cs);

@@ -69,7 +69,8 @@ def amdsmi_samples(seconds, out):
             g = j["gpu_data"][0] if isinstance(j, dict) else j[0]
             clk = {k: v["clk"]["value"] for k, v in g["clock"].items() if k.startswith("gfx_") and isinstance(v, dict)}
             pw = g["power"]["socket_power"]["value"]
-            out.append({"t": time.perf_counter(), "gfx_MHz": clk, "socket_W": pw})
+            out.append({"t": time.perf_counter(), "gfx_MHz": clk, "socket_W": pw,
+                        "throttle": g["power"].get("throttle_status")})
         except Exception as ex:  # noqa: BLE001 -- a missing tool or format change leaves this list short
             out.append({"error": str(ex)[:200]})
             return
@@ -127,18 +128,18 @@ def run_one(eng, dev, key, zero, seconds, hw):
     span_us = n_launch * k_ms * 1e3
     samp = Sampler(hw)
     smi = []
-    th = threading.Thread(target=amdsmi_samples, args=(seconds * 0.8, smi), daemon=True)
+    th = threading.Thread(target=amdsmi_samples, args=(seconds * 0.9, smi), daemon=True)
     samp.start()
     time.sleep(0.3)  # idle-ish baseline rows before the load starts
     t_load0 = samp.rows[-1][0] if samp.rows else 0.0
     eng.clock_probe(probe, wgs=16, delay_us=int(0.25 * span_us), spin_us=int(0.5 * span_us), stream=side.cuda_stream)
     eng.join()
     e0.record(stream)
+    th.start()  # amd-smi samples from the first launch on (the enqueue loop below blocks once the queue is full)
     for _ in range(n_launch):
         launch()
     eng.join()
     e1.record(stream)
-    th.start()
     torch.cuda.synchronize(dev)
     t_load1 = samp.rows[-1][0]
     time.sleep(0.3)
@@ -172,7 +173,7 @@ def run_one(eng, dev, key, zero, seconds, hw):
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--seconds", type=float, default=4.0)
+    p.add_argument("--seconds", type=float, default=8.0)
     p.add_argument("--configs", default="c2,c3,c2z,c3z,c4,c5")
     args = p.parse_args()
     import anothertls_amd as atls
