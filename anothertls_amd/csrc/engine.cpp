@@ -41,6 +41,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
                                const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
 extern "C" size_t atls_group_hdr_offset(uint32_t n_slots);
+extern "C" int atls_launch_chacha_resident(uint8_t* blk, uint32_t last, uint32_t idle_us, hipStream_t s);
 extern "C" int atls_launch_clock_probe(uint32_t wgs, uint32_t delay_us, uint32_t spin_us, uint64_t* out, hipStream_t s);
 extern "C" int atls_launch_sync_flag(const uint32_t* err, uint32_t* out, uint32_t val, hipStream_t s);
 extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t n_slots, const atls_rec* d,
@@ -681,8 +682,19 @@ struct KindEngine {
   uint64_t clock = 0;
 };
 
+// The resident ChaCha20-Poly1305 single-call server of a context (ATLS_SINGLE_RESIDENT=1, chacha.hip
+// chacha_resident): a mapped, coherent block (doorbell, flag, alive word, request, reply) and its stream.
+struct Resident {
+  uint8_t* h = nullptr;
+  uint8_t* d = nullptr;
+  hipStream_t s = nullptr;
+  int dev = -1;
+  uint32_t seq = 0;
+};
+
 struct SingleCtx {
   KindEngine kinds[4];  // AES-128, AES-192, AES-256, ChaCha20-Poly1305
+  Resident res;
   uint8_t* pin = nullptr;  // page-locked, mapped into the device's address space
   uint8_t* pin_dev = nullptr;
   size_t pin_cap = 0;
@@ -768,7 +780,9 @@ int kind_of(uint16_t suite, size_t key_len) {
 }
 
 // Slot of this key in the context's engine of its kind, installing it (LRU eviction) on a miss.
-int cached_slot(SingleCtx* c, uint16_t suite, const uint8_t* key, size_t key_len, atls_engine** eng, uint32_t* slot) {
+int cached_slot(SingleCtx* c, uint16_t suite, const uint8_t* key, size_t key_len, atls_engine** eng, uint32_t* slot,
+                bool* installed = nullptr) {
+  if (installed) *installed = false;
   KindEngine& k = c->kinds[kind_of(suite, key_len)];
   if (!k.e) {
     const char* dv = std::getenv("ATLS_DEVICE");
@@ -802,7 +816,110 @@ int cached_slot(SingleCtx* c, uint16_t suite, const uint8_t* key, size_t key_len
   if (rc) return rc;
   k.stamp[s] = ++k.clock;
   *slot = s;
+  if (installed) *installed = true;
   return ATLS_OK;
+}
+
+// ---- the resident single-call server (opt-in) ----
+bool resident_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("ATLS_SINGLE_RESIDENT");
+    return e && std::atoi(e) != 0;
+  }();
+  return v;
+}
+uint32_t resident_idle_us() {  // ATLS_SINGLE_RESIDENT_IDLE_MS: how long a server waits for the next call (20 ms)
+  static const uint32_t v = [] {
+    const char* e = std::getenv("ATLS_SINGLE_RESIDENT_IDLE_MS");
+    const long ms = e ? std::atol(e) : 20;
+    return (uint32_t)std::min<long>(std::max<long>(ms, 1), 1000) * 1000u;
+  }();
+  return v;
+}
+constexpr uint32_t kResStop = 0xffffffffu;
+constexpr size_t kResBell = 0, kResFlag = 64, kResAlive = 128, kResReq = 256, kResTag = 512, kResRes = 528,
+                 kResBytes = 1024, kResOut = 8192, kResBlock = 16384;
+struct ResidentReqH {  // chacha.hip ResidentReq
+  const void* ks;
+  atls_rec d;
+  uint32_t tag_off;
+  uint32_t open;
+};
+std::mutex& residents_mu() {
+  static std::mutex* m = new std::mutex();
+  return *m;
+}
+std::vector<Resident*>& residents() {
+  static std::vector<Resident*>* v = new std::vector<Resident*>();
+  return *v;
+}
+// At exit every server is told to stop and waited for, before the runtime unmaps the blocks they poll.
+void stop_residents() {
+  std::lock_guard<std::mutex> lk(residents_mu());
+  for (Resident* r : residents()) {
+    if (!r->h) continue;
+    __atomic_store_n((uint32_t*)(r->h + kResBell), kResStop, __ATOMIC_RELEASE);
+    (void)hipSetDevice(r->dev);
+    (void)hipStreamSynchronize(r->s);
+  }
+}
+
+// One call through the context's resident server: the request is written into the mapped block, the
+// doorbell rung, and the server (launched when it is not running, or relaunched when it left before
+// seeing the call) answers with the flag. Returns ATLS_OK or ATLS_INTERNAL_ERROR; outputs are in the block.
+// The context's block and stream (allocated on first use; the servers are stopped at exit).
+int resident_ready(SingleCtx* c, atls_engine* e) {
+  Resident& R = c->res;
+  if (!R.h) {
+    void* p = nullptr;
+    void* pd = nullptr;
+    if (hipHostMalloc(&p, kResBlock, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return ATLS_INTERNAL_ERROR;
+    if (hipHostGetDevicePointer(&pd, p, 0) != hipSuccess || hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipHostFree(p);
+      return ATLS_INTERNAL_ERROR;
+    }
+    std::memset(p, 0, kResBlock);
+    R.h = (uint8_t*)p;
+    R.d = (uint8_t*)pd;
+    R.dev = e->device;
+    std::lock_guard<std::mutex> lk(residents_mu());
+    if (residents().empty()) std::atexit(stop_residents);
+    residents().push_back(&R);
+  }
+  return ATLS_OK;
+}
+
+int resident_call(SingleCtx* c, const void* ks, const atls_rec& d, const uint8_t* bytes, uint32_t nbytes,
+                  uint32_t tag_off, bool open) {
+  Resident& R = c->res;
+  uint8_t* h = R.h;
+  const ResidentReqH q{ks, d, tag_off, open ? 1u : 0u};
+  std::memcpy(h + kResReq, &q, sizeof q);
+  std::memcpy(h + kResBytes, bytes, nbytes);
+  uint32_t v = ++R.seq;
+  if (v == kResStop || v == 0) v = R.seq = 1;
+  uint32_t* flag = (uint32_t*)(h + kResFlag);
+  uint32_t* alive = (uint32_t*)(h + kResAlive);
+  __atomic_store_n(flag, v - 1u, __ATOMIC_RELEASE);
+  __atomic_store_n((uint32_t*)(h + kResBell), v, __ATOMIC_SEQ_CST);
+  auto launch = [&] {
+    __atomic_store_n(alive, 1u, __ATOMIC_SEQ_CST);
+    return atls_launch_chacha_resident(R.d, 0u, resident_idle_us(), R.s);  // last = 0: never a call's value
+  };
+  if (__atomic_load_n(alive, __ATOMIC_SEQ_CST) == 0 && launch()) return ATLS_INTERNAL_ERROR;
+  for (uint64_t i = 1;; i++) {
+    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return ATLS_OK;
+    if ((i & 255) == 0 && __atomic_load_n(alive, __ATOMIC_ACQUIRE) == 0) {
+      // the server left (idle) before it saw this call: its flag store precedes alive := 0, so look once more
+      if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return ATLS_OK;
+      if (launch()) return ATLS_INTERNAL_ERROR;  // same stream: starts once the old one has left
+    }
+    if ((i & 4095) == 0) {
+      const hipError_t qs = hipStreamQuery(R.s);
+      if (qs != hipSuccess && qs != hipErrorNotReady) return ATLS_INTERNAL_ERROR;
+    }
+    __builtin_ia32_pause();
+  }
 }
 
 // Records up to this many bytes are read by the kernel straight from the pinned staging block
@@ -860,7 +977,8 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
   if (!c) return ATLS_INTERNAL_ERROR;
   atls_engine* e = nullptr;
   uint32_t slot = 0;
-  int rc = cached_slot(c, suite, key, key_len, &e, &slot);
+  bool installed = false;
+  int rc = cached_slot(c, suite, key, key_len, &e, &slot, &installed);
   if (rc) return rc;
   // pinned block: descriptor | tag | open result | completion flag | iv || aad | input | output
   const size_t rec_at = 0, tag_at = 64, res_at = 80, done_at = 88, aux_at = 96;
@@ -898,6 +1016,40 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
   hipStream_t s = e->stream;
+  if (inl && suite == ATLS_TLS_CHACHA20_POLY1305_SHA256 && resident_enabled()) {
+    // the resident server: no launch per call (the new key's setup, if any, finishes first)
+    if (installed && hipStreamSynchronize(s) != hipSuccess) return ATLS_INTERNAL_ERROR;
+    uint8_t bytes[atls::kSingleInline];
+    if (iv_len) std::memcpy(bytes, iv, iv_len);
+    if (aad_len) std::memcpy(bytes + iv_len, aad, aad_len);
+    if (len) std::memcpy(bytes + inl_in, in, len);
+    if (open) std::memcpy(bytes + inl_tag, tag_in, 16);
+    atls_rec d = r;
+    d.in_off = inl_in;
+    d.aux_off = 0;
+    d.out_off = 0;
+    if (resident_ready(c, e)) return ATLS_INTERNAL_ERROR;
+    uint8_t* rh = c->res.h;
+    if (open) std::memset(rh + kResRes, 0xff, sizeof(atls_open_result));  // the server writes every field
+    else std::memcpy(rh + kResTag, kTagCanary, 16);
+    rc = resident_call(c, (const atls::KeySched*)e->ks.p + slot, d, bytes, (uint32_t)(inl_tag + (open ? 16 : 0)),
+                       (uint32_t)inl_tag, open);
+    if (rc) return rc;
+    if (!open) {
+      if (std::memcmp(rh + kResTag, kTagCanary, 16) == 0) return ATLS_ILLEGAL_PARAMETER;
+      if (len) std::memcpy(out, rh + kResOut, len);
+      std::memcpy(tag_out, rh + kResTag, 16);
+      return ATLS_OK;
+    }
+    atls_open_result res;
+    std::memcpy(&res, rh + kResRes, sizeof res);
+    if (res.status != ATLS_OK) {
+      if (len) std::memset(out, 0, len);
+      return res.status;
+    }
+    if (len) std::memcpy(out, rh + kResOut, len);
+    return ATLS_OK;
+  }
   uint8_t* hd = c->pin_dev;
   const uint32_t done_val = ++c->calls;
   // the flag word holds anything after a (re)allocation of the block: set it to a value other than

@@ -3,13 +3,16 @@
 // whose one lane writes a flag into mapped pinned memory that the host spins on, (c) the same flag
 // written by hipStreamWriteValue32 behind the kernel, (d) a one-key install waited for by a stream sync
 // and by atls_engine_sync, (e) atls_seal /
-// atls_open of one record (ChaCha20-Poly1305 and AES-128-GCM, 1,537 and 16,385 B). Prints JSON.
+// atls_open of one record (ChaCha20-Poly1305 and AES-128-GCM, 1,537 and 16,385 B), (g) the round trip of a
+// resident wave polling a doorbell in mapped memory. Prints JSON. Run with ATLS_SINGLE_RESIDENT=1 the
+// ChaCha20-Poly1305 calls that fit the argument block go through the resident server.
 // Build: hipcc --offload-arch=gfx950 -O2 -Iinclude tools/single_call_floor.hip -Lanothertls_amd -latls
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -33,6 +36,32 @@ __global__ void empty_kernel_big(BigArgs a) {
   if (threadIdx.x == 0) {
     __threadfence_system();
     *(volatile uint32_t*)a.flag = a.v + a.bytes[3711];
+  }
+}
+
+// (g) a resident wave instead of a launch per call: the kernel stays on one CU polling a
+// doorbell word in mapped, coherent host memory (s_sleep between polls); for request v it reads `nbytes`
+// of request data from mapped host memory (the record a call would hand over), writes them back to a
+// mapped reply area and raises the flag to v. It leaves on the stop value, or after `idle_ms` without a
+// request -- an exit every wave reaches whatever the host does.
+__global__ void doorbell_server(const uint32_t* bell, uint32_t* flag, const uint4* req, uint4* rep, uint32_t nbytes,
+                                uint32_t idle_ms) {
+  uint32_t last = 0;
+  unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    const uint32_t v = __hip_atomic_load(bell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (v == 0xffffffffu) break;
+    if (v == last) {
+      if (__builtin_amdgcn_s_memrealtime() - t_last > 100000ull * idle_ms) break;  // 100 MHz ticks
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    last = v;
+    for (uint32_t i = threadIdx.x; i < nbytes / 16; i += blockDim.x) rep[i] = req[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    t_last = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -92,6 +121,40 @@ int main() {
   printf("{\"empty_launch_sync_us\": %.1f, \"empty_launch_flag_spin_us\": %.1f, \"empty_launch_writevalue_spin_us\": %.1f, "
          "\"empty_launch_3712B_args_flag_spin_us\": %.1f",
          sync_us, spin_us, wv_us, big_us);
+  // (g) the doorbell round trip of a resident wave: no payload, and a 1,552-byte record each way
+  {
+    uint8_t* blk = nullptr;  // [0] bell, [64] flag, [4096..] request, [8192..] reply
+    if (hipHostMalloc((void**)&blk, 16384, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) abort();
+    memset(blk, 0, 16384);
+    uint8_t* dblk = nullptr;
+    (void)hipHostGetDevicePointer((void**)&dblk, blk, 0);
+    auto* bell = (uint32_t*)blk;
+    auto* fl = (uint32_t*)(blk + 64);
+    hipStream_t ps;
+    if (hipStreamCreateWithFlags(&ps, hipStreamNonBlocking) != hipSuccess) abort();
+    for (uint32_t nb : {0u, 1552u}) {
+      __atomic_store_n(bell, 0u, __ATOMIC_RELEASE);
+      __atomic_store_n(fl, 0u, __ATOMIC_RELEASE);
+      hipLaunchKernelGGL(doorbell_server, dim3(1), dim3(64), 0, ps, (const uint32_t*)dblk, (uint32_t*)(dblk + 64),
+                         (const uint4*)(dblk + 4096), (uint4*)(dblk + 8192), nb, 2000u);
+      uint32_t v = 0;
+      const double db = median_us([&] {
+        ++v;
+        for (uint32_t i = 0; i < nb; i += 64) blk[4096 + i] = (uint8_t)v;  // the request data changes per call
+        __atomic_store_n(bell, v, __ATOMIC_RELEASE);
+        auto t0 = std::chrono::steady_clock::now();
+        while (__atomic_load_n(fl, __ATOMIC_ACQUIRE) != v) {
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) abort();  // the server left
+        }
+      }, 2000);
+      __atomic_store_n(bell, 0xffffffffu, __ATOMIC_RELEASE);
+      if (hipStreamSynchronize(ps) != hipSuccess) abort();
+      if (nb && blk[8192] != (uint8_t)v) abort();
+      printf(", \"resident_wave_doorbell_%uB_us\": %.1f", nb, db);
+    }
+    (void)hipStreamDestroy(ps);
+    (void)hipHostFree(blk);
+  }
   // (f) a new key: atls_update_keys of one AES-128 / AES-256 slot (key-setup kernel, the key in the launch
   // arguments), then a wait on the engine stream -- the end-to-end cost of a connection's new key
   for (int kl : {16, 32}) {
@@ -140,6 +203,7 @@ int main() {
              kl == 16 ? "aes128gcm" : "chacha20poly1305", n, open);
     }
   }
-  printf("}\n");
+  const char* rm = getenv("ATLS_SINGLE_RESIDENT");
+  printf(", \"single_resident\": %s}\n", rm && atoi(rm) ? "true" : "false");
   return 0;
 }
