@@ -1164,11 +1164,30 @@ __device__ __forceinline__ void q4_record(const KeySched* k, const atls_rec& d, 
 }
 #undef QRL
 
+// q4_record with the record's bytes and its output passing through LDS in 16-byte pieces: its 4-byte and byte
+// accesses straight to mapped host memory would each be a PCIe transaction (the resident server's request and
+// reply live there: 20.8 us per 1,537-B call that way). in: IV || AAD || input (|| tag), read 16 B at a time
+// (d.in_off / aux_off / tag_off index it); out + d.out_off (16-byte aligned) receives the output.
+template <bool OPEN>
+__device__ __forceinline__ void q4_staged(const KeySched* k, const atls_rec& d, const uint8_t* in, uint32_t tag_off,
+                                          uint8_t* out, uint8_t* tag_out, atls_open_result* res) {
+  __shared__ uint4 stage_in[kSingleInline / 16], stage_out[kSingleInline / 16];
+  const uint32_t t = threadIdx.x;
+  const uint32_t nin = (tag_off + (OPEN ? 16u : 0u) + 15u) / 16u, nout = (d.len + 15u) / 16u;  // <= 224 each
+  for (uint32_t i = t; i < nin; i += 256u) stage_in[i] = ld16(in + 16u * i);
+  __syncthreads();
+  atls_rec dl = d;
+  dl.out_off = 0;
+  q4_record<OPEN>(k, dl, (const uint8_t*)stage_in, tag_off, (uint8_t*)stage_out, tag_out, res);
+  __syncthreads();  // the output is whole in LDS
+  for (uint32_t i = t; i < nout; i += 256u) st16(out + d.out_off + 16u * i, stage_out[i]);
+}
+
 template <bool OPEN>
 __global__ __launch_bounds__(256) void chacha_single_q4(ChSingle) {
   const ChSingle* S = (const ChSingle*)__builtin_amdgcn_kernarg_segment_ptr();
   const ChArgs& A = S->A;
-  q4_record<OPEN>(A.ks + S->d.key_slot, S->d, S->bytes, S->tag_off, A.out, A.tags_out, A.res);
+  q4_staged<OPEN>(A.ks + S->d.key_slot, S->d, S->bytes, S->tag_off, A.out, A.tags_out, A.res);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave's stores have left
@@ -1179,55 +1198,95 @@ __global__ __launch_bounds__(256) void chacha_single_q4(ChSingle) {
 // A launch costs 5.9-6.4 us before the first instruction and after the flag (tools/single_call_floor.hip:
 // empty_launch_*_flag_spin_us); a wave that stays resident and polls a doorbell word in mapped host memory
 // answers in 1.7 us, 4.2 us with 1,552 B read from and written to mapped memory (resident_wave_doorbell_*).
-// chacha_resident is that wave's workgroup: thread 0 polls the doorbell (s_sleep between polls, the other
-// waves parked at the barrier); request v (a new value) is the ResidentReq in the block, sealed / opened by
-// q4_record with every input read from and every output written to the mapped block; then the flag := v.
-// It leaves when the doorbell holds kResidentStop or after idle_us without a request, writing alive := 0
-// as its last store -- an exit every wave reaches whatever the host does (the host stops it at exit too).
+// chacha_resident is one workgroup serving every call context of the process (a resident kernel holds its
+// hardware queue, and the process has few: one server, not one per context). The mapped block has a slot per
+// context (doorbell, flag, request, reply) and a common area (alive, stop). Lanes 0..7 of wave 0 poll the
+// slots' doorbells and flags (s_sleep between polls; the other waves wait at the barrier); a slot whose
+// doorbell differs from the value last served there holds request v = the doorbell value: its header and the
+// largest request a slot holds come into LDS in one round trip of 16-byte loads, q4_record seals / opens it
+// from LDS into LDS, the reply goes out in 16-byte stores, then the slot's flag := v. The server
+// leaves on the stop word or after idle_us without a request, writing alive := 0 as its last store -- an
+// exit every wave reaches whatever the host does (the host sets the stop word at exit).
 struct ResidentReq {
   const KeySched* ks;  // the key slot's schedule (device memory)
   atls_rec d;          // in_off / aux_off index bytes; out_off indexes the reply area
   uint32_t tag_off;
   uint32_t open;
 };
-constexpr uint32_t kResidentStop = 0xffffffffu;
-constexpr size_t kResBell = 0, kResFlag = 64, kResAlive = 128, kResReq = 256, kResTag = 512, kResRes = 528,
-                 kResBytes = 1024, kResOut = 8192, kResBlock = 16384;
-static_assert(kResBytes + kSingleInline <= kResOut && kResOut + kSingleInline + 16 <= kResBlock, "resident block");
+constexpr int kResSlots = 8;
+constexpr size_t kResBell = 0, kResFlag = 64, kResReq = 256, kResTag = 512, kResRes = 528, kResBytes = 1024,
+                 kResOut = 8192, kResSlotBytes = 16384, kResCommon = kResSlots * kResSlotBytes, kResAlive = kResCommon,
+                 kResStopAt = kResCommon + 64;
+static_assert(kResBytes + kSingleInline <= kResOut && kResOut + kSingleInline + 16 <= kResSlotBytes, "resident slot");
 
-__global__ __launch_bounds__(256) void chacha_resident(uint8_t* blk, uint32_t last, uint32_t idle_us) {
-  __shared__ uint32_t cmd;
-  uint32_t* bell = (uint32_t*)(blk + kResBell);
+__global__ __launch_bounds__(256) void chacha_resident(uint8_t* blk, uint32_t idle_us) {
+  __shared__ int cmd_slot;
+  __shared__ uint32_t cmd_v;
+  __shared__ uint4 hdr[4];  // the request (ResidentReq, 64 B)
+  __shared__ uint4 stage_in[kSingleInline / 16], stage_out[kSingleInline / 16];
+  static_assert(sizeof(ResidentReq) == sizeof(hdr), "request header");
+  const int t = (int)threadIdx.x;
+  // lane i < 8 of wave 0 keeps the last value it served for slot i (the flag the host set before this server)
+  uint32_t served = 0;
+  if (t < kResSlots)
+    served = __hip_atomic_load((uint32_t*)(blk + (size_t)t * kResSlotBytes + kResFlag), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
   for (;;) {
-    if (threadIdx.x == 0) {
+    if (t < 64) {  // wave 0: lanes 0..7 watch the slots' doorbells (one uncached load per lane and poll)
+      const uint32_t* bell = (const uint32_t*)(blk + (size_t)(t < kResSlots ? t : 0) * kResSlotBytes + kResBell);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      uint32_t v;
-      for (;;) {
-        v = __hip_atomic_load(bell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        if (v != last) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 100ull * idle_us) {
-          v = kResidentStop;  // idle: leave
+      int slot = -1;
+      uint32_t v = 0;
+      for (uint32_t it = 0;; it++) {
+        const uint32_t b = t < kResSlots ? __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+        const unsigned long long m = __ballot(t < kResSlots && b != 0u && b != served);
+        if (m) {
+          slot = __builtin_ffsll((long long)m) - 1;
+          v = (uint32_t)__shfl((int)b, slot, 64);
           break;
+        }
+        if ((it & 15u) == 15u) {
+          const uint32_t stop = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load((uint32_t*)(blk + kResStopAt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+          if (stop || __builtin_amdgcn_s_memrealtime() - t0 > 100ull * idle_us) break;  // told to stop, or idle
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      cmd = v;
+      if (t == 0) {
+        cmd_slot = slot;
+        cmd_v = v;
+      }
+      if (slot >= 0 && t == slot) served = v;
     }
     __syncthreads();
-    const uint32_t v = cmd;
-    __syncthreads();  // every wave has read cmd before thread 0 may overwrite it
-    if (v == kResidentStop) break;
+    const int slot = cmd_slot;
+    const uint32_t v = cmd_v;
+    if (slot < 0) break;
+    uint8_t* sl = blk + (size_t)slot * kResSlotBytes;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request the host wrote before the doorbell
-    const ResidentReq R = *(const ResidentReq*)(blk + kResReq);
-    if (R.open) q4_record<true>(R.ks, R.d, blk + kResBytes, R.tag_off, blk + kResOut, blk + kResTag, (atls_open_result*)(blk + kResRes));
-    else q4_record<false>(R.ks, R.d, blk + kResBytes, R.tag_off, blk + kResOut, blk + kResTag, (atls_open_result*)(blk + kResRes));
+    // header and every byte a request can hold, in one round trip (the request's own size is in the header)
+    if (t < (int)(kSingleInline / 16)) stage_in[t] = ((const uint4*)(sl + kResBytes))[t];
+    else if (t < (int)(kSingleInline / 16) + 4) hdr[t - kSingleInline / 16] = ((const uint4*)(sl + kResReq))[t - kSingleInline / 16];
+    __syncthreads();  // (also: every wave has read the command before wave 0 may overwrite it)
+    ResidentReq R;
+    __builtin_memcpy(&R, hdr, sizeof R);
+    atls_rec dl = R.d;
+    dl.out_off = 0;
+    if (R.open)
+      q4_record<true>(R.ks, dl, (const uint8_t*)stage_in, R.tag_off, (uint8_t*)stage_out, sl + kResTag,
+                      (atls_open_result*)(sl + kResRes));
+    else
+      q4_record<false>(R.ks, dl, (const uint8_t*)stage_in, R.tag_off, (uint8_t*)stage_out, sl + kResTag,
+                       (atls_open_result*)(sl + kResRes));
+    __syncthreads();  // the reply is whole in LDS
+    const uint32_t nout = (R.d.len + 15u) / 16u;
+    for (uint32_t i = (uint32_t)t; i < nout; i += 256u) ((uint4*)(sl + kResOut))[i] = stage_out[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();  // every wave's stores have left
-    if (threadIdx.x == 0) __hip_atomic_store((uint32_t*)(blk + kResFlag), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    last = v;
+    if (t == 0) __hip_atomic_store((uint32_t*)(sl + kResFlag), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     __hip_atomic_store((uint32_t*)(blk + kResAlive), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -1296,8 +1355,8 @@ extern "C" int atls_launch_chacha_single(int open, const void* ks, uint32_t n_sl
 }
 
 // The resident single-call server on stream s (chacha_resident): blk = the mapped block's device address.
-extern "C" int atls_launch_chacha_resident(uint8_t* blk, uint32_t last, uint32_t idle_us, hipStream_t s) {
-  hipLaunchKernelGGL(atls::chacha_resident, dim3(1), dim3(256), 0, s, blk, last, idle_us);
+extern "C" int atls_launch_chacha_resident(uint8_t* blk, uint32_t idle_us, hipStream_t s) {
+  hipLaunchKernelGGL(atls::chacha_resident, dim3(1), dim3(256), 0, s, blk, idle_us);
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
 

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <chrono>
@@ -41,7 +42,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
                                const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
 extern "C" size_t atls_group_hdr_offset(uint32_t n_slots);
-extern "C" int atls_launch_chacha_resident(uint8_t* blk, uint32_t last, uint32_t idle_us, hipStream_t s);
+extern "C" int atls_launch_chacha_resident(uint8_t* blk, uint32_t idle_us, hipStream_t s);
 extern "C" int atls_launch_clock_probe(uint32_t wgs, uint32_t delay_us, uint32_t spin_us, uint64_t* out, hipStream_t s);
 extern "C" int atls_launch_sync_flag(const uint32_t* err, uint32_t* out, uint32_t val, hipStream_t s);
 extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t n_slots, const atls_rec* d,
@@ -419,10 +420,13 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   return finish(e, 0, true);
 }
 
+void resident_yield();  // below, with the resident single-call server
+
 int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
               void* out, uint8_t* tags_out, const uint8_t* tags_in, atls_open_result* res, uint32_t flags) {
   if (!e) return ATLS_INTERNAL_ERROR;
   if (n == 0) return ATLS_OK;
+  resident_yield();
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
   if (e->n_slots == 0) return ATLS_ILLEGAL_PARAMETER;
@@ -615,6 +619,7 @@ int key_status(const atls_key& k) {
 // (the table grows, keeping the other slots); replace = the table becomes exactly these n slots.
 // Caller holds e->mu.
 int install_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t n, bool replace) {
+  resident_yield();
   int status = ATLS_OK;
   for (uint32_t i = 0; i < n && status == ATLS_OK; i++) status = key_status(keys[i]);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
@@ -682,19 +687,10 @@ struct KindEngine {
   uint64_t clock = 0;
 };
 
-// The resident ChaCha20-Poly1305 single-call server of a context (ATLS_SINGLE_RESIDENT=1, chacha.hip
-// chacha_resident): a mapped, coherent block (doorbell, flag, alive word, request, reply) and its stream.
-struct Resident {
-  uint8_t* h = nullptr;
-  uint8_t* d = nullptr;
-  hipStream_t s = nullptr;
-  int dev = -1;
-  uint32_t seq = 0;
-};
-
 struct SingleCtx {
   KindEngine kinds[4];  // AES-128, AES-192, AES-256, ChaCha20-Poly1305
-  Resident res;
+  int res_slot = -2;    // slot of the resident single-call server (-2: not asked yet, -1: none left)
+  uint32_t res_seq = 0;
   uint8_t* pin = nullptr;  // page-locked, mapped into the device's address space
   uint8_t* pin_dev = nullptr;
   size_t pin_cap = 0;
@@ -836,87 +832,139 @@ uint32_t resident_idle_us() {  // ATLS_SINGLE_RESIDENT_IDLE_MS: how long a serve
   }();
   return v;
 }
-constexpr uint32_t kResStop = 0xffffffffu;
-constexpr size_t kResBell = 0, kResFlag = 64, kResAlive = 128, kResReq = 256, kResTag = 512, kResRes = 528,
-                 kResBytes = 1024, kResOut = 8192, kResBlock = 16384;
+// The process's resident ChaCha20-Poly1305 single-call server (ATLS_SINGLE_RESIDENT=1, chacha.hip
+// chacha_resident): one mapped, coherent block with a slot per call context (doorbell, flag, request, reply)
+// and a common area (alive, stop), one stream, one workgroup -- a resident kernel holds a hardware queue,
+// so there is one server for the whole process, not one per context.
+constexpr int kResSlots = 8;
+constexpr size_t kResBell = 0, kResFlag = 64, kResReq = 256, kResTag = 512, kResRes = 528, kResBytes = 1024,
+                 kResOut = 8192, kResSlotBytes = 16384, kResCommon = kResSlots * kResSlotBytes, kResAlive = kResCommon,
+                 kResStopAt = kResCommon + 64, kResBlock = kResCommon + 4096;
 struct ResidentReqH {  // chacha.hip ResidentReq
   const void* ks;
   atls_rec d;
   uint32_t tag_off;
   uint32_t open;
 };
-std::mutex& residents_mu() {
-  static std::mutex* m = new std::mutex();
-  return *m;
+struct ResidentServer {
+  std::mutex mu;
+  uint8_t* h = nullptr;
+  uint8_t* d = nullptr;
+  hipStream_t s = nullptr;
+  int dev = -1;
+  int slots_used = 0;
+  bool failed = false;
+};
+ResidentServer& resident_server() {
+  static ResidentServer* r = new ResidentServer();  // never destroyed: stopped by stop_resident at exit
+  return *r;
 }
-std::vector<Resident*>& residents() {
-  static std::vector<Resident*>* v = new std::vector<Resident*>();
-  return *v;
-}
-// At exit every server is told to stop and waited for, before the runtime unmaps the blocks they poll.
-void stop_residents() {
-  std::lock_guard<std::mutex> lk(residents_mu());
-  for (Resident* r : residents()) {
-    if (!r->h) continue;
-    __atomic_store_n((uint32_t*)(r->h + kResBell), kResStop, __ATOMIC_RELEASE);
-    (void)hipSetDevice(r->dev);
-    (void)hipStreamSynchronize(r->s);
-  }
+// At exit the server is told to stop and waited for, before the runtime unmaps the block it polls.
+void stop_resident() {
+  ResidentServer& S = resident_server();
+  std::lock_guard<std::mutex> lk(S.mu);
+  if (!S.h) return;
+  __atomic_store_n((uint32_t*)(S.h + kResStopAt), 1u, __ATOMIC_SEQ_CST);
+  (void)hipSetDevice(S.dev);
+  (void)hipStreamSynchronize(S.s);
 }
 
-// One call through the context's resident server: the request is written into the mapped block, the
-// doorbell rung, and the server (launched when it is not running, or relaunched when it left before
-// seeing the call) answers with the flag. Returns ATLS_OK or ATLS_INTERNAL_ERROR; outputs are in the block.
-// The context's block and stream (allocated on first use; the servers are stopped at exit).
-int resident_ready(SingleCtx* c, atls_engine* e) {
-  Resident& R = c->res;
-  if (!R.h) {
+// The context's slot of the server (allocating the server on first use): -1 when every slot is taken,
+// the server failed, or the call runs on another device.
+int resident_slot(SingleCtx* c, atls_engine* e) {
+  if (c->res_slot != -2) return c->res_slot;
+  ResidentServer& S = resident_server();
+  std::lock_guard<std::mutex> lk(S.mu);
+  c->res_slot = -1;
+  if (S.failed) return -1;
+  if (!S.h) {
     void* p = nullptr;
     void* pd = nullptr;
-    if (hipHostMalloc(&p, kResBlock, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return ATLS_INTERNAL_ERROR;
-    if (hipHostGetDevicePointer(&pd, p, 0) != hipSuccess || hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking) != hipSuccess) {
+    if (hipHostMalloc(&p, kResBlock, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+      S.failed = true;
+      return -1;
+    }
+    if (hipHostGetDevicePointer(&pd, p, 0) != hipSuccess || hipStreamCreateWithFlags(&S.s, hipStreamNonBlocking) != hipSuccess) {
       (void)hipHostFree(p);
-      return ATLS_INTERNAL_ERROR;
+      S.failed = true;
+      return -1;
     }
     std::memset(p, 0, kResBlock);
-    R.h = (uint8_t*)p;
-    R.d = (uint8_t*)pd;
-    R.dev = e->device;
-    std::lock_guard<std::mutex> lk(residents_mu());
-    if (residents().empty()) std::atexit(stop_residents);
-    residents().push_back(&R);
+    S.h = (uint8_t*)p;
+    S.d = (uint8_t*)pd;
+    S.dev = e->device;
+    std::atexit(stop_resident);
   }
-  return ATLS_OK;
+  if (S.dev != e->device || S.slots_used >= kResSlots) return -1;
+  c->res_slot = S.slots_used++;
+  return c->res_slot;
 }
 
-int resident_call(SingleCtx* c, const void* ks, const atls_rec& d, const uint8_t* bytes, uint32_t nbytes,
-                  uint32_t tag_off, bool open) {
-  Resident& R = c->res;
-  uint8_t* h = R.h;
+// A running server holds its hardware queue (GPU_MAX_HW_QUEUES is 4 per process), so any other kernel of the
+// process whose stream maps to that queue would wait for the server's idle timeout: before a launch of its
+// own, the process stops the server (stop word, wait for alive == 0, clear the word); the next resident call
+// starts it again.
+void resident_yield() {
+  if (!resident_enabled()) return;
+  ResidentServer& S = resident_server();
+  if (!S.h || __atomic_load_n((const uint32_t*)(S.h + kResAlive), __ATOMIC_SEQ_CST) == 0) return;
+  std::lock_guard<std::mutex> lk(S.mu);
+  uint32_t* alive = (uint32_t*)(S.h + kResAlive);
+  uint32_t* stop = (uint32_t*)(S.h + kResStopAt);
+  if (__atomic_load_n(alive, __ATOMIC_SEQ_CST) == 0) return;
+  __atomic_store_n(stop, 1u, __ATOMIC_SEQ_CST);
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(alive, __ATOMIC_ACQUIRE) != 0 && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
+    __builtin_ia32_pause();
+  (void)hipStreamSynchronize(S.s);  // the kernel itself has ended
+  __atomic_store_n(alive, 0u, __ATOMIC_SEQ_CST);
+  __atomic_store_n(stop, 0u, __ATOMIC_SEQ_CST);
+}
+
+// Launches the server unless it runs (caller holds S.mu). The kernel's last store is alive := 0, so a
+// server seen alive == 0 is gone or about to be; a new one on the same stream starts after it.
+int resident_launch_locked(ResidentServer& S) {
+  if (__atomic_load_n((uint32_t*)(S.h + kResAlive), __ATOMIC_SEQ_CST) != 0) return ATLS_OK;
+  __atomic_store_n((uint32_t*)(S.h + kResAlive), 1u, __ATOMIC_SEQ_CST);
+  return atls_launch_chacha_resident(S.d, resident_idle_us(), S.s);
+}
+
+// One call through the server: request into the context's slot, doorbell, then the slot's flag. Returns
+// ATLS_OK (outputs in the slot) or ATLS_INTERNAL_ERROR.
+int resident_call(SingleCtx* c, const void* ks, const atls_rec& d, const uint8_t* bytes, uint32_t nbytes, uint32_t tag_off,
+                  bool open) {
+  ResidentServer& S = resident_server();
+  uint8_t* h = S.h + (size_t)c->res_slot * kResSlotBytes;
   const ResidentReqH q{ks, d, tag_off, open ? 1u : 0u};
   std::memcpy(h + kResReq, &q, sizeof q);
   std::memcpy(h + kResBytes, bytes, nbytes);
-  uint32_t v = ++R.seq;
-  if (v == kResStop || v == 0) v = R.seq = 1;
+  uint32_t v = ++c->res_seq;
+  if (v == 0) v = c->res_seq = 1;
   uint32_t* flag = (uint32_t*)(h + kResFlag);
-  uint32_t* alive = (uint32_t*)(h + kResAlive);
-  __atomic_store_n(flag, v - 1u, __ATOMIC_RELEASE);
+  const uint32_t* alive = (const uint32_t*)(S.h + kResAlive);
+  __atomic_store_n(flag, v - 1u, __ATOMIC_RELEASE);  // pending: doorbell != flag
   __atomic_store_n((uint32_t*)(h + kResBell), v, __ATOMIC_SEQ_CST);
-  auto launch = [&] {
-    __atomic_store_n(alive, 1u, __ATOMIC_SEQ_CST);
-    return atls_launch_chacha_resident(R.d, 0u, resident_idle_us(), R.s);  // last = 0: never a call's value
-  };
-  if (__atomic_load_n(alive, __ATOMIC_SEQ_CST) == 0 && launch()) return ATLS_INTERNAL_ERROR;
+  if (__atomic_load_n(alive, __ATOMIC_SEQ_CST) == 0) {
+    std::lock_guard<std::mutex> lk(S.mu);
+    if (resident_launch_locked(S)) return ATLS_INTERNAL_ERROR;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t i = 1;; i++) {
     if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return ATLS_OK;
     if ((i & 255) == 0 && __atomic_load_n(alive, __ATOMIC_ACQUIRE) == 0) {
-      // the server left (idle) before it saw this call: its flag store precedes alive := 0, so look once more
+      // the server left (idle) before it saw this call: its flag stores precede alive := 0, so look once more
       if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return ATLS_OK;
-      if (launch()) return ATLS_INTERNAL_ERROR;  // same stream: starts once the old one has left
+      std::lock_guard<std::mutex> lk(S.mu);
+      if (resident_launch_locked(S)) return ATLS_INTERNAL_ERROR;
     }
     if ((i & 4095) == 0) {
-      const hipError_t qs = hipStreamQuery(R.s);
+      const hipError_t qs = hipStreamQuery(S.s);
       if (qs != hipSuccess && qs != hipErrorNotReady) return ATLS_INTERNAL_ERROR;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        std::fprintf(stderr, "anothertls_amd: resident server did not answer in 2 s (slot %d bell %u flag %u alive %u)\n",
+                     c->res_slot, v, __atomic_load_n(flag, __ATOMIC_ACQUIRE), __atomic_load_n(alive, __ATOMIC_ACQUIRE));
+        return ATLS_INTERNAL_ERROR;
+      }
     }
     __builtin_ia32_pause();
   }
@@ -1016,7 +1064,7 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
   hipStream_t s = e->stream;
-  if (inl && suite == ATLS_TLS_CHACHA20_POLY1305_SHA256 && resident_enabled()) {
+  if (inl && suite == ATLS_TLS_CHACHA20_POLY1305_SHA256 && resident_enabled() && resident_slot(c, e) >= 0) {
     // the resident server: no launch per call (the new key's setup, if any, finishes first)
     if (installed && hipStreamSynchronize(s) != hipSuccess) return ATLS_INTERNAL_ERROR;
     uint8_t bytes[atls::kSingleInline];
@@ -1028,8 +1076,7 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
     d.in_off = inl_in;
     d.aux_off = 0;
     d.out_off = 0;
-    if (resident_ready(c, e)) return ATLS_INTERNAL_ERROR;
-    uint8_t* rh = c->res.h;
+    uint8_t* rh = resident_server().h + (size_t)c->res_slot * kResSlotBytes;
     if (open) std::memset(rh + kResRes, 0xff, sizeof(atls_open_result));  // the server writes every field
     else std::memcpy(rh + kResTag, kTagCanary, 16);
     rc = resident_call(c, (const atls::KeySched*)e->ks.p + slot, d, bytes, (uint32_t)(inl_tag + (open ? 16 : 0)),
@@ -1050,6 +1097,7 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
     if (len) std::memcpy(out, rh + kResOut, len);
     return ATLS_OK;
   }
+  resident_yield();
   uint8_t* hd = c->pin_dev;
   const uint32_t done_val = ++c->calls;
   // the flag word holds anything after a (re)allocation of the block: set it to a value other than
@@ -1244,6 +1292,7 @@ int atls_open(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t*
 int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, size_t secret_len, uint32_t n,
                      atls_key* out_keys) {
   if (!e) return ATLS_INTERNAL_ERROR;
+  resident_yield();
   if (suite != ATLS_TLS_AES_128_GCM_SHA256 && suite != ATLS_TLS_AES_256_GCM_SHA384 &&
       suite != ATLS_TLS_CHACHA20_POLY1305_SHA256)
     return ATLS_INSUFFICIENT_SECURITY;
@@ -1265,6 +1314,7 @@ int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, siz
 int atls_hash_batch(atls_engine* e, int op, uint32_t hash_len, const uint8_t* data, size_t data_len,
                     const atls_span* keys, const atls_span* msgs, uint32_t n, uint32_t out_len, uint8_t* out) {
   if (!e) return ATLS_INTERNAL_ERROR;
+  resident_yield();
   if ((hash_len != 32 && hash_len != 48) || op < ATLS_HASH_SHA || op > ATLS_HASH_HKDF_EXPAND || !msgs ||
       (op != ATLS_HASH_SHA && !keys))
     return ATLS_ILLEGAL_PARAMETER;
@@ -1296,6 +1346,7 @@ int atls_hash_batch(atls_engine* e, int op, uint32_t hash_len, const uint8_t* da
 int atls_key_schedule(atls_engine* e, uint32_t hash_len, const uint8_t* shared, size_t shared_len,
                       const uint8_t* hello_hashes, const uint8_t* handshake_hashes, uint32_t n, uint8_t* out) {
   if (!e) return ATLS_INTERNAL_ERROR;
+  resident_yield();
   if ((hash_len != 32 && hash_len != 48) || !shared || !hello_hashes || shared_len > 1024) return ATLS_ILLEGAL_PARAMETER;
   if (n == 0) return ATLS_OK;
   std::lock_guard<std::mutex> lk(e->mu);
@@ -1320,6 +1371,7 @@ int atls_key_schedule(atls_engine* e, uint32_t hash_len, const uint8_t* shared, 
 int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* in, void* out, size_t nblocks,
                     uint32_t flags) {
   if (!e) return ATLS_INTERNAL_ERROR;
+  resident_yield();
   if (nblocks == 0) return ATLS_OK;
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;

@@ -49,6 +49,13 @@ namespace atls {
 #ifndef ATLS_CTR_CACHE
 #define ATLS_CTR_CACHE 1
 #endif
+#ifndef ATLS_GEN_MASK
+#define ATLS_GEN_MASK 1  // a general step runs its AES rounds and GHASH product only on the lanes whose slot lies in the
+                         // record (EXEC-masked LDS lookups; a C2 record's last step has 4 such lanes of 64). Same-box
+                         // A/B, 3 rounds, parity first (profiles/r05/ab_genmask*.log): C5 seal 0.3175-0.321 -> 0.3148-
+                         // 0.319 ms, open -1 %; C4 -0.3 %; C2 with a key per record unchanged (1.311-1.317 ms) at a
+                         // 2 % higher clock. 0 = every lane
+#endif
 
 #ifndef ATLS_GCM_FAST_FIRST
 #define ATLS_GCM_FAST_FIRST 0  // 1: a TLS record's first step (E_K(J0), AAD, 62 data blocks) without the general step's
@@ -633,6 +640,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     const uint64_t t_l = __builtin_amdgcn_s_memtime();
     t_ld += t_l - t_step;
 #endif
+    const bool live = !ATLS_GEN_MASK || s <= m;  // ATLS_GEN_MASK: lanes past the record skip the AES and GHASH work
     if (use_cache) {  // ctr = 1 for slots 0..na, else 1 + s - na: the step's ctr >> 8 is lane 63's
       const uint32_t ctr = cb[3];
       uint32_t hi;
@@ -642,8 +650,8 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
         const uint32_t sl = base + LN - 1u;
         hi = (j0[3] + (sl > na ? sl - na : 0u)) >> 8;
       }
-      aes_cached(st, perm((ctr & 0xffu) ^ k15, lb, 0x0c0c0400u), hi);
-    } else {
+      if (live) aes_cached(st, perm((ctr & 0xffu) ^ k15, lb, 0x0c0c0400u), hi);
+    } else if (live) {
       aes_encrypt_tt<NR>(st, rk, rkr, lb);
     }
 #ifdef ATLS_TT_STAMPS
@@ -700,7 +708,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     }
     // Y <- Y * H^64 ^ B on the lanes that hold a GHASH block; the others keep Y (s_last below).
     uint32_t yn[4] = {y[0], y[1], y[2], y[3]};
-    if (base && !(ATLS_DBG_SKIP & 8)) ghash_mul<ATLS_GHASH_W>(yn, wh);  // Y = 0 before the first step
+    if (base && !(ATLS_DBG_SKIP & 8) && live) ghash_mul<ATLS_GHASH_W>(yn, wh);  // Y = 0 before the first step
     if (s >= 1 && s <= m) {
 #pragma unroll
       for (int w = 0; w < 4; w++) y[w] = yn[w] ^ B[w];

@@ -77,7 +77,7 @@ def parse():
     p.add_argument("--sustain-s", type=float, default=5.0,
                    help="after the timed steps, seal the headline batch back to back for this long (every rank) "
                         "and report the sustained rate (clocks under continuous load); 0 = skip")
-    p.add_argument("--c1-threads", type=int, default=8, help="C1 at scale: worker threads per stream batch")
+    p.add_argument("--c1-threads", type=int, default=16, help="C1 at scale: worker threads per stream batch")
     p.add_argument("--dry-run-cap", type=int, default=64,
                    help="--dry-run: content bytes per record of the whole-batch exchange rehearsal")
     p.add_argument("--dry-run", action="store_true",

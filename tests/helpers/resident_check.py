@@ -36,9 +36,13 @@ def main():
     rng = random.Random(0x5E5)
     c = atls.CipherSuite(0x1303).get_cipher()
     keys = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(3)]
+    print("first call", flush=True)
+    one(c, rng, keys[0], 1537, 5)
+    print("first call OK", flush=True)
     for aad_len in (0, 5, 40):
         for n in (0, 1, 15, 16, 63, 64, 65, 127, 128, 1023, 1024, 1536, 1537, 3000, 3455, 3456, 3500, 3600, 16385):
             one(c, rng, keys[n % 3], n, aad_len)
+        print("aad", aad_len, "OK", flush=True)
     for _ in range(3):  # the server leaves after ATLS_SINGLE_RESIDENT_IDLE_MS without a call; the next call relaunches it
         time.sleep(0.05)
         one(c, rng, keys[0], 1537, 5)

@@ -14,10 +14,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.timeout(240)
+@pytest.mark.timeout(150)
 def test_resident_single_calls_vs_oracle():
     env = dict(os.environ, ATLS_SINGLE_RESIDENT="1", ATLS_SINGLE_RESIDENT_IDLE_MS="5")
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "helpers", "resident_check.py")], env=env,
-                         capture_output=True, text=True, timeout=200)
+                         capture_output=True, text=True, timeout=90)
     assert out.returncode == 0, (out.stdout[-2000:], out.stderr[-3000:])
     assert "resident OK" in out.stdout

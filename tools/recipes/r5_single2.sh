@@ -1,15 +1,11 @@
 #!/bin/bash
-# Round 5: the ChaCha20-Poly1305 single call -- four lanes per block (chacha_single_q4) and the opt-in resident
-# server (ATLS_SINGLE_RESIDENT=1): parity tests, then the C-ABI latency floors with and without the server.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
-O=gpurun_out/r5sc; mkdir -p $O
+O=gpurun_out/r5sc2; mkdir -p $O
 timeout -k 10 500 python -u -m pytest tests/test_gpu_single_resident.py tests/test_gpu_single_call.py -x -v --timeout 300 --timeout-method thread > $O/gpu_tests_single.txt 2>&1 || { tail -40 $O/gpu_tests_single.txt; exit 1; }
 tail -1 $O/gpu_tests_single.txt
 timeout -k 10 200 ./tools/single_call_floor > $O/single_call_floor.json 2>&1 || { tail -5 $O/single_call_floor.json; exit 1; }
 cat $O/single_call_floor.json
 ATLS_SINGLE_RESIDENT=1 timeout -k 10 200 ./tools/single_call_floor > $O/single_call_floor_resident.json 2>&1 || { tail -5 $O/single_call_floor_resident.json; exit 1; }
 cat $O/single_call_floor_resident.json
-PARITY=1 VARIANTS="base mask" CONFIGS="c5_mixed_256Ki_x_64B-16KiB c4_aes256gcm_1Mi_x_16KiB" ROUNDS=3 timeout -k 10 1200 bash tools/recipes/r5_ab.sh genmask || exit 1
-PARITY=0 VARIANTS="base mask" CONFIGS="c2_aes128gcm_64Ki_x_16KiB" BENCH_ARGS="--key-slots 65536" ROUNDS=3 timeout -k 10 600 bash tools/recipes/r5_ab.sh genmask_keyrec || exit 1
