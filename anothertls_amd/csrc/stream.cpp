@@ -18,7 +18,9 @@
 //
 // Throughput (round 5): the host work around the device batch is copies and socket
 // calls, so the batch keeps them few and spreads them over worker threads (atls_sb_set_threads):
-//   * a write is copied once, into the batch's page-locked input arena the seal batch reads;
+//   * a write is copied once, into the batch's page-locked input arena the seal batch reads; a flush takes
+//     that arena and seals and sends from it outside the batch lock, so writes for the next flush (another
+//     thread's) fill the second arena meanwhile;
 //   * flush sends the connections' slices of the page-locked wire buffer from T threads;
 //   * atls_sb_recv_all receives on every connection from T threads, straight into each connection's
 //     receive buffer, where the whole records are found in place (record_split.h scan_records);
@@ -56,6 +58,25 @@ constexpr int kBrokenPipe = 254;                  // TlsError::BrokenPipe, alert
 constexpr size_t kRecvChunk = size_t(256) << 10;  // room made in a receive buffer per recv call
 constexpr size_t kRxMax = size_t(1) << 31;        // unopened bytes per connection (record offsets are u32)
 constexpr int kMaxThreads = 64;
+// A flush or receive round goes to the engine in batches of whole connections of at most this many wire
+// bytes (one connection more than that is a batch of its own): the page-locked staging the batches use stays
+// bounded however much is queued, and a flush sends one batch while the engine seals the next.
+constexpr size_t kBatchBytes = size_t(64) << 20;
+
+// [c0, c1) ranges of connections whose wire bytes (prefix sums `base`) fit kBatchBytes, skipping empty ones
+std::vector<std::pair<size_t, size_t>> batch_groups(const std::vector<size_t>& base) {
+  std::vector<std::pair<size_t, size_t>> g;
+  const size_t nc = base.size() - 1;
+  for (size_t c0 = 0; c0 < nc;) {
+    while (c0 < nc && base[c0 + 1] == base[c0]) c0++;
+    if (c0 == nc) break;
+    size_t c1 = c0 + 1;
+    while (c1 < nc && base[c1 + 1] - base[c0] <= kBatchBytes) c1++;
+    g.emplace_back(c0, c1);
+    c0 = c1;
+  }
+  return g;
+}
 
 // Grow-only page-locked host buffer: the engine's copies from it run at full PCIe speed. keep: bytes
 // [0, keep) survive a growth (the write arena fills across several writes).
@@ -185,12 +206,16 @@ struct atls_stream_batch {
   std::vector<atls_key> keys;  // 2 slots per connection
   bool keys_dirty = false;
   std::vector<Conn> conns;
-  Pinned in, wire, pt;
-  size_t in_len = 0;  // bytes of queued writes in `in`
-  std::vector<atls_rec> recs;
+  // writes go to arena in[cur]; a flush takes that arena (cur flips) and seals and sends from it without the
+  // batch lock, so the next flush's writes fill the other arena meanwhile (flush_mu: one flush at a time, so an
+  // arena is never written while a flush still reads it)
+  Pinned in[2], wire_out[2], wire, pt;
+  int cur = 0;
+  size_t in_len = 0;  // bytes of queued writes in in[cur]
+  std::vector<atls_rec> recs, frecs;  // open / flush descriptors
   std::vector<atls_open_result> res;
   int threads = 1;
-  std::mutex mu;
+  std::mutex mu, flush_mu;
   // env ATLS_SB_PROFILE=1: seconds per phase, printed to stderr by atls_sb_destroy
   bool profile = std::getenv("ATLS_SB_PROFILE") != nullptr;
   double t_write = 0, t_seal = 0, t_send = 0, t_recv = 0, t_poll = 0, t_gather = 0, t_open = 0, t_hand = 0;
@@ -236,42 +261,35 @@ void publish_err(Conn& c) {
   if (c.err && !c.inbox->err) c.inbox->err = c.err;
 }
 
-long open_pending_locked(atls_stream_batch* sb) {
-  const size_t nc = sb->conns.size();
-  std::vector<size_t> wbase(nc + 1, 0), rbase(nc + 1, 0);
-  for (size_t i = 0; i < nc; i++) {
-    const Conn& c = sb->conns[i];
-    const bool any = !c.err && !c.offs.empty();
-    wbase[i + 1] = wbase[i] + (any ? c.rx_done : 0);
-    rbase[i + 1] = rbase[i] + (any ? c.offs.size() : 0);
-  }
-  const size_t n = rbase[nc], wire_bytes = wbase[nc];
-  if (n == 0) return 0;
-  if (n > 0xffffffffu) return -ATLS_ILLEGAL_PARAMETER;
-  int rc = install_keys(sb);
-  if (rc) return -rc;
+// Opens the whole records of connections [c0, c1) (wire offsets `wbase`, record counts `rbase`, both prefix
+// sums from c0) in one engine batch and hands each connection its plaintexts.
+long open_group(atls_stream_batch* sb, size_t c0, size_t c1, const std::vector<size_t>& wbase,
+                const std::vector<size_t>& rbase) {
+  const size_t n = rbase[c1] - rbase[c0], wire_bytes = wbase[c1] - wbase[c0];
   // plaintexts packed back to back (the engine copies a gapless output range back in one piece)
   if (!sb->wire.reserve(wire_bytes + 16) || !sb->pt.reserve(wire_bytes + 16)) return -ATLS_INTERNAL_ERROR;
-  std::vector<size_t> pbase(nc + 1, 0);
-  for (size_t i = 0; i < nc; i++) {
+  std::vector<size_t> pbase(c1 - c0 + 1, 0);
+  for (size_t i = c0; i < c1; i++) {
     size_t ptb = 0;
     const Conn& c = sb->conns[i];
     if (rbase[i + 1] != rbase[i])
       for (uint32_t o : c.offs) ptb += (((size_t)c.rx[o + 3] << 8) | c.rx[o + 4]) - 16;
-    pbase[i + 1] = pbase[i] + ptb;
+    pbase[i - c0 + 1] = pbase[i - c0] + ptb;
   }
   sb->recs.assign(n, atls_rec{});
   sb->res.assign(n, atls_open_result{});
   Stopwatch sw;
-  parallel(sb->threads, nc, [&](size_t ci) {  // gather each connection's whole records, describe them
+  parallel(sb->threads, c1 - c0, [&](size_t k) {  // gather each connection's whole records, describe them
+    const size_t ci = c0 + k;
     Conn& c = sb->conns[ci];
     if (rbase[ci + 1] == rbase[ci]) return;
-    std::memcpy(sb->wire.p + wbase[ci], c.rx.data(), c.rx_done);
-    size_t po = pbase[ci];
+    const size_t wb = wbase[ci] - wbase[c0], rb = rbase[ci] - rbase[c0];
+    std::memcpy(sb->wire.p + wb, c.rx.data(), c.rx_done);
+    size_t po = pbase[k];
     for (size_t j = 0; j < c.offs.size(); j++) {
       const uint8_t* h = c.rx.data() + c.offs[j];
-      atls_rec& d = sb->recs[rbase[ci] + j];
-      d.in_off = wbase[ci] + c.offs[j];
+      atls_rec& d = sb->recs[rb + j];
+      d.in_off = wb + c.offs[j];
       d.out_off = po;
       po += (((uint32_t)h[3] << 8) | h[4]) - 16;
       d.seq = c.rseq + j;
@@ -281,21 +299,24 @@ long open_pending_locked(atls_stream_batch* sb) {
     }
   });
   sb->t_gather += sw.lap();
-  rc = atls_open_batch(sb->e, sb->recs.data(), (uint32_t)n, sb->wire.p, nullptr, nullptr, sb->pt.p, sb->res.data(), 0);
+  const int rc = atls_open_batch(sb->e, sb->recs.data(), (uint32_t)n, sb->wire.p, nullptr, nullptr, sb->pt.p,
+                                 sb->res.data(), 0);
   if (rc) return -rc;
   sb->t_open += sw.lap();
-  parallel(sb->threads, nc, [&](size_t ci) {  // hand each connection its plaintexts, keep its partial tail
+  parallel(sb->threads, c1 - c0, [&](size_t k) {  // hand each connection its plaintexts, keep its partial tail
+    const size_t ci = c0 + k;
     Conn& c = sb->conns[ci];
     if (rbase[ci + 1] == rbase[ci]) return;
+    const size_t rb = rbase[ci] - rbase[c0];
     std::vector<Record> got;
     got.reserve(c.offs.size());
     for (size_t j = 0; j < c.offs.size(); j++) {
-      const atls_open_result& r = sb->res[rbase[ci] + j];
+      const atls_open_result& r = sb->res[rb + j];
       if (r.status) {  // a failed record ends the connection
         c.err = r.status;
         break;
       }
-      const uint8_t* p = sb->pt.p + sb->recs[rbase[ci] + j].out_off;
+      const uint8_t* p = sb->pt.p + sb->recs[rb + j].out_off;
       got.push_back(Record{r.content_type, std::vector<uint8_t>(p, p + r.content_len)});
     }
     c.rseq += c.offs.size();
@@ -310,6 +331,27 @@ long open_pending_locked(atls_stream_batch* sb) {
     }
   });
   sb->t_hand += sw.lap();
+  return (long)n;
+}
+
+long open_pending_locked(atls_stream_batch* sb) {
+  const size_t nc = sb->conns.size();
+  std::vector<size_t> wbase(nc + 1, 0), rbase(nc + 1, 0);
+  for (size_t i = 0; i < nc; i++) {
+    const Conn& c = sb->conns[i];
+    const bool any = !c.err && !c.offs.empty();
+    wbase[i + 1] = wbase[i] + (any ? c.rx_done : 0);
+    rbase[i + 1] = rbase[i] + (any ? c.offs.size() : 0);
+  }
+  const size_t n = rbase[nc];
+  if (n == 0) return 0;
+  if (n > 0xffffffffu) return -ATLS_ILLEGAL_PARAMETER;
+  const int rc = install_keys(sb);
+  if (rc) return -rc;
+  for (const auto& g : batch_groups(wbase)) {  // a connection that has records pending has wire bytes
+    const long got = open_group(sb, g.first, g.second, wbase, rbase);
+    if (got < 0) return got;
+  }
   return (long)n;
 }
 
@@ -391,8 +433,9 @@ int atls_sb_write(atls_stream_batch* sb, int conn, uint8_t content_type, const u
     Stopwatch& w;
     ~Add() { sb->t_write += w.lap(); }
   } add{sb, sw};
-  if (!sb->in.reserve(sb->in_len + len + 16, sb->in_len)) return ATLS_INTERNAL_ERROR;
-  if (len) std::memcpy(sb->in.p + sb->in_len, data, len);  // the only copy of the write on the host
+  Pinned& in = sb->in[sb->cur];
+  if (!in.reserve(sb->in_len + len + 16, sb->in_len)) return ATLS_INTERNAL_ERROR;
+  if (len) std::memcpy(in.p + sb->in_len, data, len);  // the only copy of the write on the host
   if (len == 0) c.out.push_back(Queued{sb->in_len, 0, content_type});
   for (size_t off = 0; off < len; off += kMaxFragment)
     c.out.push_back(Queued{sb->in_len + off, (uint32_t)std::min(kMaxFragment, len - off), content_type});
@@ -402,54 +445,102 @@ int atls_sb_write(atls_stream_batch* sb, int conn, uint8_t content_type, const u
 
 long atls_sb_flush(atls_stream_batch* sb) {
   if (!sb) return -ATLS_INTERNAL_ERROR;
-  std::lock_guard<std::mutex> lk(sb->mu);
-  const size_t nc = sb->conns.size();
-  std::vector<size_t> wbase(nc + 1, 0), rbase(nc + 1, 0);
-  for (size_t i = 0; i < nc; i++) {
-    size_t bytes = 0;
-    for (const Queued& r : sb->conns[i].out) bytes += r.len + 22;  // header 5, inner type 1, tag 16
-    wbase[i + 1] = wbase[i] + bytes;
-    rbase[i + 1] = rbase[i] + sb->conns[i].out.size();
+  std::lock_guard<std::mutex> fl(sb->flush_mu);
+  // under the batch lock: take every connection's queued records and the arena they are in
+  std::vector<int> fds;
+  std::vector<char> dead;
+  std::vector<size_t> wbase, rbase;
+  size_t n = 0;
+  Pinned* arena = nullptr;
+  int threads = 1;
+  {
+    std::lock_guard<std::mutex> lk(sb->mu);
+    const size_t nc = sb->conns.size();
+    rbase.assign(nc + 1, 0);
+    wbase.assign(nc + 1, 0);
+    for (size_t i = 0; i < nc; i++) {
+      size_t bytes = 0;
+      for (const Queued& r : sb->conns[i].out) bytes += r.len + 22;  // header 5, inner type 1, tag 16
+      wbase[i + 1] = wbase[i] + bytes;
+      rbase[i + 1] = rbase[i] + sb->conns[i].out.size();
+    }
+    n = rbase[nc];
+    if (n == 0) return 0;
+    if (n > 0xffffffffu) return -ATLS_ILLEGAL_PARAMETER;
+    const int rc = install_keys(sb);
+    if (rc) return -rc;
+    sb->frecs.assign(n, atls_rec{});
+    fds.resize(nc);
+    dead.assign(nc, 0);
+    for (size_t ci = 0; ci < nc; ci++) {  // each connection's records back to back on its wire slice
+      Conn& c = sb->conns[ci];
+      fds[ci] = c.fd;
+      dead[ci] = c.err != 0;
+      size_t wo = wbase[ci];
+      for (size_t j = 0; j < c.out.size(); j++) {
+        const Queued& r = c.out[j];
+        atls_rec& d = sb->frecs[rbase[ci] + j];
+        d.in_off = r.in_off;
+        d.out_off = wo;  // made relative to its engine batch below
+        d.seq = c.wseq + j;
+        d.len = r.len;
+        d.key_slot = c.wslot;
+        d.content_type = r.type;
+        d.mode = ATLS_MODE_WIRE;
+        wo += r.len + 22;
+      }
+      c.wseq += c.out.size();
+      c.out.clear();
+    }
+    arena = &sb->in[sb->cur];
+    sb->cur ^= 1;  // later writes fill the other arena, sized once like this one so writes do not regrow it
+    sb->in_len = 0;
+    if (!sb->in[sb->cur].reserve(arena->cap)) return -ATLS_INTERNAL_ERROR;
+    threads = sb->threads;
   }
-  const size_t n = rbase[nc];
-  if (n == 0) return 0;
-  if (n > 0xffffffffu) return -ATLS_ILLEGAL_PARAMETER;
-  int rc = install_keys(sb);
-  if (rc) return -rc;
-  if (!sb->wire.reserve(wbase[nc] + 16)) return -ATLS_INTERNAL_ERROR;
-  sb->recs.assign(n, atls_rec{});
-  for (size_t ci = 0; ci < nc; ci++) {  // each connection's records back to back on its wire slice
-    const Conn& c = sb->conns[ci];
-    size_t wo = wbase[ci];
-    uint64_t seq = c.wseq;
-    for (size_t j = 0; j < c.out.size(); j++) {
-      const Queued& r = c.out[j];
-      atls_rec& d = sb->recs[rbase[ci] + j];
-      d.in_off = r.in_off;
-      d.out_off = wo;
-      d.seq = seq++;
-      d.len = r.len;
-      d.key_slot = c.wslot;
-      d.content_type = r.type;
-      d.mode = ATLS_MODE_WIRE;
-      wo += r.len + 22;
+  // engine batches of whole connections; batch g is sealed into wire_out[g & 1] while batch g - 1 is sent
+  // from the other buffer (a connection's records are all in one batch, and batches go out in order)
+  const size_t nc = fds.size();
+  std::vector<char> failed(nc, 0);
+  const auto groups = batch_groups(wbase);
+  std::thread sender;
+  int rc = ATLS_OK;
+  size_t g = 0;
+  Stopwatch sw;
+  for (; g < groups.size(); g++) {
+    const size_t c0 = groups[g].first, c1 = groups[g].second;
+    Pinned& out = sb->wire_out[g & 1];
+    if (!out.reserve(wbase[c1] - wbase[c0] + 16)) {
+      rc = ATLS_INTERNAL_ERROR;
+      break;
+    }
+    for (size_t r = rbase[c0]; r < rbase[c1]; r++) sb->frecs[r].out_off -= wbase[c0];
+    rc = atls_seal_batch(sb->e, sb->frecs.data() + rbase[c0], (uint32_t)(rbase[c1] - rbase[c0]), arena->p, nullptr,
+                         out.p, nullptr, 0);
+    if (rc) break;
+    sb->t_seal += sw.lap();
+    if (sender.joinable()) sender.join();
+    sender = std::thread([&, c0, c1, wire = out.p] {
+      parallel(threads, c1 - c0, [&](size_t k) {
+        const size_t ci = c0 + k;
+        if (dead[ci] || wbase[ci + 1] == wbase[ci]) return;
+        if (!send_all(fds[ci], wire + wbase[ci] - wbase[c0], wbase[ci + 1] - wbase[ci])) failed[ci] = 1;
+      });
+    });
+  }
+  if (sender.joinable()) sender.join();
+  sb->t_send += sw.lap();
+  {
+    std::lock_guard<std::mutex> lk(sb->mu);
+    for (size_t ci = 0; ci < nc; ci++) {
+      Conn& c = sb->conns[ci];
+      if (failed[ci] && !c.err) c.err = kBrokenPipe;
+      // records of batches the engine did not seal are lost: their connections end with the engine's error
+      if (rc && g < groups.size() && ci >= groups[g].first && wbase[ci + 1] != wbase[ci] && !c.err) c.err = rc;
+      publish_err(c);
     }
   }
-  Stopwatch sw;
-  rc = atls_seal_batch(sb->e, sb->recs.data(), (uint32_t)n, sb->in.p, nullptr, sb->wire.p, nullptr, 0);
-  if (rc) return -rc;
-  sb->t_seal += sw.lap();
-  sb->in_len = 0;
-  parallel(sb->threads, nc, [&](size_t ci) {
-    Conn& c = sb->conns[ci];
-    if (c.out.empty()) return;
-    c.wseq += c.out.size();
-    c.out.clear();
-    if (!c.err && !send_all(c.fd, sb->wire.p + wbase[ci], wbase[ci + 1] - wbase[ci])) c.err = kBrokenPipe;
-  });
-  sb->t_send += sw.lap();
-  for (Conn& c : sb->conns) publish_err(c);
-  return (long)n;
+  return rc ? -rc : (long)n;
 }
 
 int atls_sb_feed(atls_stream_batch* sb, int conn, const uint8_t* data, size_t len) {

@@ -74,6 +74,10 @@ def parse():
     p.add_argument("--settle-ms", type=float, default=200.0,
                    help="before the warm-up steps, time the on-device copy rate for this long (it also brings the "
                         "GPU's clock up from idle, which a few 1-ms warm-up steps do not; 0 = after the steps)")
+    p.add_argument("--load-settle-ms", type=float, default=300.0,
+                   help="then run the config's own seals back to back for this long before the warm-up steps: the "
+                        "clock under this load settles over ~100 ms (DESIGN §6), so the timed steps see the steady "
+                        "state a serving engine runs at (untimed; 0 = off)")
     p.add_argument("--sustain-s", type=float, default=5.0,
                    help="after the timed steps, seal the headline batch back to back for this long (every rank) "
                         "and report the sustained rate (clocks under continuous load); 0 = skip")
@@ -431,7 +435,7 @@ def lds_roofline(batch, kern_ms, sclk_mhz, cus):
 
 
 def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_slots=None, keep=False,
-            settle_ms=0.0):
+            settle_ms=0.0, load_settle_ms=0.0):
     """This rank's shard of config `name`, device-resident: `steps` timed seals (barrier + sync on both
     sides, max over ranks) with the kernels' interval from HIP events on the engine stream, then as many
     opens of the sealed records with every status, length and (uniform configs) plaintext byte checked.
@@ -452,6 +456,16 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
     d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
     torch.cuda.synchronize(dev)
     copy_gbps = copy_probe(d_in, d_out, settle_ms) if settle_ms > 0 else None
+    flags0 = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC | (atls.FLAG_LAZY_JOIN if lazy else 0)
+    if load_settle_ms > 0:
+        # the same seals back to back, untimed, until the clock has settled under this load: a C2 launch takes
+        # 1.29-1.46 ms for the first few after other work, ~1.0 ms after ~100 ms
+        ptrs = [t.data_ptr() for t in (d_recs, d_in, d_aux, d_out, d_tags)]
+        t_end = time.perf_counter() + load_settle_ms * 1e-3
+        while time.perf_counter() < t_end:
+            for _ in range(8):
+                eng.seal_batch(ptrs[0], ptrs[1], ptrs[2], ptrs[3], ptrs[4], flags=flags0, n=n)
+            eng.sync()
     # LAZY_JOIN: a mixed batch's ChaCha20-Poly1305 kernel is not joined back at the end of each step,
     # so the next step's plan and AES-GCM kernel start beside it (C5); no effect on one-suite batches
     flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC | (atls.FLAG_LAZY_JOIN if lazy else 0)
@@ -582,7 +596,8 @@ def main():
     eng = atls.Engine(local)
     # this rank's shard of the config's record stream (weak scaling: fixed records per GPU)
     m = measure(args.config, eng, dev, rank, world, args.steps, args.warmup, not args.no_lazy_join,
-                records=args.records, key_slots=args.key_slots, keep=True, settle_ms=args.settle_ms)
+                records=args.records, key_slots=args.key_slots, keep=True, settle_ms=args.settle_ms,
+                load_settle_ms=args.load_settle_ms)
     batch, recs, n, payload = m["batch"], m["batch"]["recs"], m["n"], m["payload"]
     d_in, d_out, d_tags, d_aux = m["d_in"], m["d_out"], m["d_tags"], m["d_aux"]
     flags, stream, sync, kern_ms, achieved, alg_bytes = m["flags"], m["stream"], m["sync"], m["kern_ms"], m["achieved"], m["alg_bytes"]
@@ -745,14 +760,16 @@ def main():
         for name in EXTRA_CONFIGS:
             if name == args.config:
                 continue
-            mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join, settle_ms=args.settle_ms)
+            mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join, settle_ms=args.settle_ms,
+                         load_settle_ms=args.load_settle_ms)
             cfgs[name] = config_summary(name, mm, steps)
             del mm
         if not args.key_slots:
             # SURVEY §8(d)'s worst case: C2 with a key per record (65,536 connections), so no lane groups form
             name = "c2_aes128gcm_64Ki_x_16KiB"
             mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join,
-                         key_slots=workload.CONFIGS[name][1], settle_ms=args.settle_ms)
+                         key_slots=workload.CONFIGS[name][1], settle_ms=args.settle_ms,
+                         load_settle_ms=args.load_settle_ms)
             cfgs[name + " (a key per record)"] = config_summary(name, mm, steps)
             del mm
         if world == 1 and not args.records:
@@ -760,14 +777,16 @@ def main():
             # device-resident launch -- what the 8-GPU config's root holds before it scatters
             name = "c4_aes256gcm_1Mi_x_16KiB"
             mm = measure(name, eng, dev, rank, world, min(steps, 5), min(warmup, 1), not args.no_lazy_join,
-                         records=workload.CONFIGS[name][1], settle_ms=args.settle_ms)
+                         records=workload.CONFIGS[name][1], settle_ms=args.settle_ms,
+                         load_settle_ms=args.load_settle_ms)
             cfgs[name + " (whole batch, 1 GPU)"] = config_summary(name, mm, min(steps, 5))
             del mm
             torch.cuda.empty_cache()
             # C5 likewise: the whole 256 Ki-record mixed batch (2.16 GB each way) in one planned launch
             name = "c5_mixed_256Ki_x_64B-16KiB"
             mm = measure(name, eng, dev, rank, world, steps, warmup, not args.no_lazy_join,
-                         records=workload.CONFIGS[name][1], settle_ms=args.settle_ms)
+                         records=workload.CONFIGS[name][1], settle_ms=args.settle_ms,
+                         load_settle_ms=args.load_settle_ms)
             cfgs[name + " (whole batch, 1 GPU)"] = config_summary(name, mm, steps)
             del mm
             torch.cuda.empty_cache()

@@ -206,7 +206,10 @@ def test_native_stream_batch_threads(atls):
 
 
 @pytest.mark.timeout(120)
-@pytest.mark.parametrize("conns,threads", [(4, 1), (16, 4)])
+# (80, 8): 80 connections x 2 bodies is 168 MB of wire per flush and per receive round at most, so both go
+# to the engine in several batches of whole connections (stream.cpp kBatchBytes, 64 MiB), sealed while the
+# previous batch is sent
+@pytest.mark.parametrize("conns,threads", [(4, 1), (16, 4), (80, 8)])
 def test_c1_native_loopback_tool(atls, conns, threads):
     exe = os.path.join(ROOT, "tools", "c1_loopback_native")
     if not os.path.exists(exe):

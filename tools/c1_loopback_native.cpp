@@ -8,7 +8,9 @@
 // With threads > 1 (C1 at scale) both batches use that many worker threads
 // (atls_sb_set_threads): the server's flush sends from T threads; the client receives every connection
 // with atls_sb_recv_all, opens everything pending in one batch, and T reader threads take the opened
-// records of their connections (atls_sb_read_ready) and compare every byte.
+// records of their connections (atls_sb_read_ready) and compare every byte; the server writes the next bodies
+// on one thread while another flushes the last ones. phase_ms: each side's time per phase over the timed run
+// (the two sides overlap, so they do not sum to wall).
 //
 // Built by __graft_entry__.build() with tools/build_native.sh (g++, linked to libatls.so).
 // Usage: tools/c1_loopback_native [reps=8] [conns=1] [threads=1]
@@ -19,6 +21,8 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -92,14 +96,58 @@ int main(int argc, char** argv) {
     cc[i] = atls_sb_add_connection(cs, c, &key, &key);
   }
   std::atomic<bool> ok{true};
+  using clk = std::chrono::steady_clock;
+  auto secs = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
+  double t_write = 0, t_flush = 0, t_recv = 0, t_open = 0, t_read = 0;  // phase seconds of the last run
+  long flushes = 0, rounds = 0;  // server flushes and client receive rounds of the last run
   auto run = [&](int n) {
+    t_write = t_flush = t_recv = t_open = t_read = 0;
+    flushes = rounds = 0;
+    auto write_rep = [&] {
+      const auto t = clk::now();
+      for (int i = 0; i < conns; i++)
+        for (int k = 0; k < kRecords; k++)  // one tls_write per 16 KiB record
+          atls_sb_write(ss, sc[i], 23, body.data() + k * kContent, kContent);
+      t_write += secs(t);
+    };
+    auto flush = [&] {
+      const auto t = clk::now();
+      if (atls_sb_flush(ss) < 0) ok = false;
+      t_flush += secs(t);
+    };
     std::thread server([&] {
-      for (int r = 0; r < n; r++) {
-        for (int i = 0; i < conns; i++)
-          for (int k = 0; k < kRecords; k++)  // one tls_write per 16 KiB record
-            atls_sb_write(ss, sc[i], 23, body.data() + k * kContent, kContent);
-        if (atls_sb_flush(ss) < 0) ok = false;
+      if (threads <= 1) {  // write a body on every connection, flush, repeat
+        for (int r = 0; r < n; r++) {
+          write_rep();
+          flush();
+          flushes++;
+        }
+        return;
       }
+      // at scale: one thread writes the next bodies while another seals and sends the last ones (a flush
+      // takes the queued records and their input arena, so writes go on into the other arena meanwhile)
+      std::mutex m;
+      std::condition_variable cv;
+      int written = 0;
+      std::thread writer([&] {
+        for (int r = 0; r < n; r++) {
+          write_rep();
+          std::lock_guard<std::mutex> lk(m);
+          written = r + 1;
+          cv.notify_one();
+        }
+      });
+      for (int flushed = 0; flushed < n;) {
+        {
+          std::unique_lock<std::mutex> lk(m);
+          cv.wait(lk, [&] { return written > flushed; });
+          flushed = written;
+        }
+        flush();
+        flushes++;
+      }
+      writer.join();
+      flush();  // anything written after the last counted body (none when reps were counted in order)
     });
     if (threads <= 1) {  // the reference's shape: one tls_read per record, in order
       std::vector<uint8_t> buf(kContent);
@@ -116,11 +164,17 @@ int main(int argc, char** argv) {
       long remaining = (long)n * kRecords * conns;
       auto t_idle = std::chrono::steady_clock::now();
       while (remaining > 0 && ok) {
+        auto t = clk::now();
+        rounds++;
         const long got = atls_sb_recv_all(cs, 100);
+        t_recv += secs(t);
+        t = clk::now();
         if (got < 0 || atls_sb_open_pending(cs) < 0) {
           ok = false;
           break;
         }
+        t_open += secs(t);
+        t = clk::now();
         std::atomic<long> taken{0};
         std::vector<std::thread> rd;
         for (int t = 0; t < threads; t++)
@@ -141,6 +195,7 @@ int main(int argc, char** argv) {
               }
           });
         for (auto& th : rd) th.join();
+        t_read += secs(t);
         remaining -= taken.load();
         if (got > 0 || taken.load() > 0) t_idle = std::chrono::steady_clock::now();
         else if (std::chrono::steady_clock::now() - t_idle > std::chrono::seconds(20)) ok = false;  // stalled
@@ -148,14 +203,20 @@ int main(int argc, char** argv) {
     }
     server.join();
   };
-  run(1);  // warm-up: device buffers, code objects, pinned staging
+  // warm-up at the timed size: device buffers, code objects and the page-locked arenas grow to what the
+  // timed run's batches need (a flush or receive round can take several bodies at once), as in a server that
+  // has been running
+  run(reps);
   const auto t0 = std::chrono::steady_clock::now();
   run(reps);
   const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   std::printf("{\"config\": \"c1_server_https_loopback_1MiB\", \"impl\": \"native atls_stream_batch\", "
               "\"suite\": \"TLS_AES_128_GCM_SHA256\", \"records_per_body\": %d, \"conns\": %d, \"reps\": %d, "
-              "\"threads\": %d, \"verified\": %s, \"gpu_MBps\": %.1f}\n",
-              kRecords, conns, reps, threads, ok.load() ? "true" : "false", (double)reps * conns * kBody / dt / 1e6);
+              "\"threads\": %d, \"verified\": %s, \"gpu_MBps\": %.1f, \"phase_ms\": {\"server_write\": %.1f, "
+              "\"server_flush\": %.1f, \"client_recv\": %.1f, \"client_open\": %.1f, \"client_read\": %.1f, "
+              "\"wall\": %.1f}, \"flushes\": %ld, \"client_rounds\": %ld}\n",
+              kRecords, conns, reps, threads, ok.load() ? "true" : "false", (double)reps * conns * kBody / dt / 1e6,
+              t_write * 1e3, t_flush * 1e3, t_recv * 1e3, t_open * 1e3, t_read * 1e3, dt * 1e3, flushes, rounds);
   for (int fd : fds) close(fd);
   atls_sb_destroy(ss);
   atls_sb_destroy(cs);
