@@ -247,14 +247,15 @@ def run_c1(args):
               "config": {"workload": C1, "records_per_body": c1.N_REC, "record_content": c1.CONTENT,
                          "suite": "TLS_AES_128_GCM_SHA256", "path": "anothertls_amd.stream.StreamBatch (WIRE mode)"}}
     # C1 at scale: the native batched socket path (tools/c1_loopback_native, atls_sb_* with
-    # worker threads) over 64 and 256 connections, every byte checked by the tool
+    # worker threads) over 64 and 256 connections, every byte checked by the tool; the server and client sides
+    # run in one process, so T threads per side is 2T on the host's CPU share (16 on the GPU box)
     exe = os.path.join(ROOT, "tools", "c1_loopback_native")
     if os.path.exists(exe):
         import subprocess
 
         scale = []
-        for conns, reps in ((64, 8), (256, 2)):
-            for threads in (1, args.c1_threads):
+        for conns, reps in ((64, 16), (256, 4)):
+            for threads in sorted({1, 8, args.c1_threads}):
                 out = subprocess.run([exe, str(reps), str(conns), str(threads)], capture_output=True, text=True,
                                      timeout=300)
                 line = json.loads(out.stdout.strip().splitlines()[-1]) if out.returncode == 0 and out.stdout.strip() \
@@ -262,8 +263,10 @@ def run_c1(args):
                 line.pop("config", None)
                 scale.append(line)
         result["at_scale"] = {"runs": scale, "unit": "MB/s of response body, seal -> 127.0.0.1 TCP -> open, every byte checked",
-                              "path": "native atls_stream_batch, one WIRE seal batch per flush and one open batch per "
-                                      "receive round, T worker threads (atls_sb_set_threads)"}
+                              "path": "native atls_stream_batch: a flush seals its records in engine batches of <= 64 MiB "
+                                      "while the previous batch is sent, a receive round opens in such batches; "
+                                      "T worker threads per batch (atls_sb_set_threads); the server writes the "
+                                      "next body while the last is flushed"}
     if not args.no_cpu_baseline:
         t = c1_cpu_reference(body, 1)
         result["cpu_baseline"] = {"value": round(len(body) / t / 1e6, 3), "unit": "MB/s", "cores": 1,

@@ -126,15 +126,21 @@ int main(int argc, char** argv) {
       }
       // at scale: one thread writes the next bodies while another seals and sends the last ones (a flush
       // takes the queued records and their input arena, so writes go on into the other arena meanwhile)
+      // The writer stays at most one body ahead of the flushes (back-pressure, as a server bounds what it
+      // queues), so a flush takes one or two bodies and the two input arenas keep their size.
       std::mutex m;
       std::condition_variable cv;
-      int written = 0;
+      int written = 0, taken = 0;
       std::thread writer([&] {
         for (int r = 0; r < n; r++) {
+          {
+            std::unique_lock<std::mutex> lk(m);
+            cv.wait(lk, [&] { return taken >= r - 1; });
+          }
           write_rep();
           std::lock_guard<std::mutex> lk(m);
           written = r + 1;
-          cv.notify_one();
+          cv.notify_all();
         }
       });
       for (int flushed = 0; flushed < n;) {
@@ -145,6 +151,9 @@ int main(int argc, char** argv) {
         }
         flush();
         flushes++;
+        std::lock_guard<std::mutex> lk(m);
+        taken = flushed;
+        cv.notify_all();
       }
       writer.join();
       flush();  // anything written after the last counted body (none when reps were counted in order)

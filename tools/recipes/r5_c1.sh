@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r5c1; mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_stream_native.py > $O/gpu_tests_stream.txt 2>&1 || { tail -30 $O/gpu_tests_stream.txt; exit 1; }
 tail -1 $O/gpu_tests_stream.txt
-for a in "8 64 1" "8 64 8" "8 64 16" "16 64 16" "2 256 16" "4 256 16"; do
+for a in ${C1_RUNS:-"8 64 1" "8 64 8" "8 64 16" "16 64 8" "16 64 16" "2 256 8" "2 256 16" "4 256 8" "4 256 16"}; do
   timeout -k 10 120 tools/c1_loopback_native $a || exit 1
 done > $O/c1_scale.log 2>&1
 cat $O/c1_scale.log
