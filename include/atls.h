@@ -261,8 +261,9 @@ void atls_partition(const atls_rec* recs, uint32_t n, int open, uint32_t parts, 
 /* ---- Batched record streams (TlsStream::tls_write / tls_read, net/stream.rs:32-150) -------
  * Many connections over one engine: atls_sb_write queues a connection's records (fragmented at
  * 2^14 bytes, RFC 8446 §5.1; the data is copied once, into the batch's page-locked input), atls_sb_flush
- * seals the queued records of every connection in one ATLS_MODE_WIRE batch and send()s each connection's
- * wire bytes; received bytes (atls_sb_recv / atls_sb_recv_all from the sockets, or atls_sb_feed) are
+ * seals the queued records of every connection in ATLS_MODE_WIRE batches of whole connections (<= 64 MiB of
+ * wire bytes each, one sealed while the previous one is sent) and send()s each connection's wire bytes in
+ * order; received bytes (atls_sb_recv / atls_sb_recv_all from the sockets, or atls_sb_feed) are
  * split into whole records (Record::from_raw, record.rs:81-102), atls_sb_open_pending opens every
  * connection's complete records in one batch, atls_sb_read returns the next application-data record of a
  * connection (blocking: receives and opens as needed; UnexpectedMessage (10) for other content types,
@@ -273,7 +274,11 @@ void atls_partition(const atls_rec* recs, uint32_t n, int open, uint32_t parts, 
  * Threads: atls_sb_set_threads(sb, T) (1..64, default 1) spreads flush's sends, atls_sb_recv_all's
  * receives and open_pending's gather / hand-over over T threads (by connection). Calls on one batch
  * are serialised, except atls_sb_read_ready (and the copy-out of atls_sb_read), which take only the
- * connection's own lock: readers of different connections copy out in parallel. */
+ * connection's own lock: readers of different connections copy out in parallel; and atls_sb_flush, which
+ * holds the batch lock only while it takes the queued records (and their input arena: later writes go to a
+ * second one), so atls_sb_write on other threads proceeds while it seals and sends (one flush at a time).
+ * If the engine fails part-way through a flush, the connections whose records were not sent end with its
+ * error. */
 typedef struct atls_stream_batch atls_stream_batch;
 enum { ATLS_WOULD_BLOCK = 253 }; /* atls_sb_read_ready: no opened record yet (not a TlsError) */
 atls_stream_batch* atls_sb_create(atls_engine* e);
