@@ -40,6 +40,8 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, int iters) {
         if (OP == 12) asm volatile("v_pk_lshlrev_b16 %0, 1, %0" : "+v"(a[i]));
         if (OP == 13) asm volatile("v_lshrrev_b32 %0, 25, %0" : "+v"(a[i]));
         if (OP == 14) { if (i < 8) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(f[i]) : "v"(fb)); }
+        if (OP == 16) asm volatile("v_xor_b32_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0" : "+v"(a[i]) : "v"(b));
+        if (OP == 17) asm volatile("v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_0" : "+v"(a[i]) : "v"(b));
         if (OP == 15) { uint64_t t = ((uint64_t)a[(i + 1) & 15] << 32) | a[i];
                         asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(t) : "v"(b), "v"(c)); a[i] = (uint32_t)t; a[(i + 1) & 15] = (uint32_t)(t >> 32); }
       }
@@ -60,14 +62,25 @@ __device__ __forceinline__ uint32_t rot16_pk(uint32_t x) {
 }
 template <int MODE>
 __device__ __forceinline__ uint32_t rot16(uint32_t x) { return MODE == 1 ? rot16_pk(x) : rot_ab(x, 16); }
+// rotl16(d ^ a) as two SDWA xors (VOP2 encodings): the low half from the high halves, the high from the low
+__device__ __forceinline__ uint32_t xrot16_sdwa(uint32_t d, uint32_t a) {
+  uint32_t t;
+  asm("v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:WORD_1\n\t"
+      "v_xor_b32_sdwa %0, %1, %2 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
+      : "=&v"(t) : "v"(d), "v"(a));
+  return t;
+}
+template <int MODE>
+__device__ __forceinline__ uint32_t xrot16(uint32_t d, uint32_t a) { return MODE == 2 ? xrot16_sdwa(d, a) : rot16<MODE>(d ^ a); }
 
 #define QR(M, a, b, c, d)                  \
-  a += b; d = rot16<M>(d ^ a);              \
+  a += b; d = xrot16<M>(d, a);              \
   c += d; b = rot_ab(b ^ c, 12);            \
   a += b; d = rot_ab(d ^ a, 8);             \
   c += d; b = rot_ab(b ^ c, 7);
 
-// MODE 0: alignbit rotations; MODE 1: rotl16 as a packed half swap.
+// MODE 0: alignbit rotations; MODE 1: rotl16 as a packed half swap; MODE 2 (round 5): rotl16(d ^ a) as two
+// SDWA xors.
 template <int MODE, int MINW>
 __global__ __launch_bounds__(256, MINW) void chacha_k(uint32_t* out, int iters) {
   uint32_t x[16], y[16];
@@ -140,9 +153,12 @@ int main() {
   run<11>("bfi_b32");
   run<12>("pk_lshlrev16");
   run<15>("mad_u64_acc");
+  run<16>("xor_sdwa_w1");
+  run<17>("add_sdwa_w1w0");
   for (int w : {2, 3}) {
     run_chacha<0, 2>("chacha alignbit", w);
     run_chacha<1, 2>("chacha rot16 pk_add", w);
+    run_chacha<2, 2>("chacha rot16 sdwa", w);
   }
   return 0;
 }
