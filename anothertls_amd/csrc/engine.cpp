@@ -304,6 +304,21 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
     const long mb = v ? std::atol(v) : 32;
     return (size_t)(mb > 0 ? mb : 32) << 20;
   }();
+  // The pipeline fills with small chunks and drains with small chunks: the first chunk's upload and the
+  // last chunk's download overlap nothing, so chunk k holds at most kFirst << k bytes on the way up and at
+  // most half of what is left on the way down (never below kFirst). ATLS_CHUNK_FIRST_MB overrides; 0 = flat.
+  static const size_t kFirst = [] {
+    const char* v = std::getenv("ATLS_CHUNK_FIRST_MB");
+    const long mb = v ? std::atol(v) : 4;
+    return (size_t)(mb > 0 ? mb : 0) << 20;
+  }();
+  const size_t in_total = n ? recs[n - 1].in_off + rec_in_len(recs[n - 1], open) : 0;
+  auto chunk_limit = [&](size_t k, size_t from) {
+    if (!kFirst) return kChunkBytes;
+    size_t lim = k < 16 ? std::min(kChunkBytes, kFirst << k) : kChunkBytes;
+    const size_t rem = in_total > from ? in_total - from : 0;
+    return std::min(lim, std::max(kFirst, rem / 2));
+  };
   auto ilen = [&](const atls_rec& r) { return rec_in_len(r, open); };
   auto olen = [&](const atls_rec& r) { return rec_out_len(r, open); };
   for (uint32_t i = 1; i < n; i++)
@@ -368,7 +383,8 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   size_t k = 0;
   for (uint32_t a = 0; a < n; k++) {
     uint32_t b = a + 1;
-    while (b < n && recs[b - 1].in_off + ilen(recs[b - 1]) - recs[a].in_off < kChunkBytes) b++;
+    const size_t lim = chunk_limit(k, recs[a].in_off);
+    while (b < n && recs[b].in_off + ilen(recs[b]) - recs[a].in_off <= lim) b++;
     while (e->pev.size() < 2 * (k + 1)) {
       hipEvent_t ev;
       if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return fail(ATLS_INTERNAL_ERROR);
