@@ -469,6 +469,9 @@ long atls_sb_flush(atls_stream_batch* sb) {
     if (n > 0xffffffffu) return -ATLS_ILLEGAL_PARAMETER;
     const int rc = install_keys(sb);
     if (rc) return -rc;
+    // the arena later writes will fill, sized like this one so they do not regrow it (before anything is taken,
+    // so a failure leaves the queued records where they are)
+    if (!sb->in[sb->cur ^ 1].reserve(sb->in[sb->cur].cap)) return -ATLS_INTERNAL_ERROR;
     sb->frecs.assign(n, atls_rec{});
     fds.resize(nc);
     dead.assign(nc, 0);
@@ -493,9 +496,8 @@ long atls_sb_flush(atls_stream_batch* sb) {
       c.out.clear();
     }
     arena = &sb->in[sb->cur];
-    sb->cur ^= 1;  // later writes fill the other arena, sized once like this one so writes do not regrow it
+    sb->cur ^= 1;  // later writes fill the other arena
     sb->in_len = 0;
-    if (!sb->in[sb->cur].reserve(arena->cap)) return -ATLS_INTERNAL_ERROR;
     threads = sb->threads;
   }
   // engine batches of whole connections; batch g is sealed into wire_out[g & 1] while batch g - 1 is sent
