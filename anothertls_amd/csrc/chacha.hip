@@ -19,6 +19,7 @@
 // ATLS_CHACHA_W2=0/1, 3 waves per SIMD), chacha_kernel<OPEN, true> (planned mixed batches beside the
 // AES-GCM kernel, 128 VGPRs), chacha_kernel_lat (the single call, one record per wave at 64 lanes).
 // Bytes per record (roofline): read L, write L + 16.
+#include "chacha_q4.h"
 #include "plan.h"
 
 namespace atls {
@@ -26,119 +27,6 @@ namespace atls {
 #ifndef ATLS_CHACHA_SHORT
 #define ATLS_CHACHA_SHORT 4096  // records up to this length take 4 lanes each, longer ones 16
 #endif
-constexpr uint32_t M26 = 0x3ffffffu;
-
-struct P130 { uint32_t l[5]; };
-
-__device__ __forceinline__ P130 p_zero() { P130 z; for (int i = 0; i < 5; i++) z.l[i] = 0; return z; }
-
-// d += h * r (unreduced 64-bit column sums; 2^130 = 5 mod p folds the high columns back with 5 r).
-__device__ __forceinline__ void p_mac(uint64_t (&d)[5], const P130& h, const P130& r) {
-  const uint32_t s1 = r.l[1] * 5, s2 = r.l[2] * 5, s3 = r.l[3] * 5, s4 = r.l[4] * 5;
-  const uint64_t h0 = h.l[0], h1 = h.l[1], h2 = h.l[2], h3 = h.l[3], h4 = h.l[4];
-  d[0] += h0 * r.l[0] + h1 * s4 + h2 * s3 + h3 * s2 + h4 * s1;
-  d[1] += h0 * r.l[1] + h1 * r.l[0] + h2 * s4 + h3 * s3 + h4 * s2;
-  d[2] += h0 * r.l[2] + h1 * r.l[1] + h2 * r.l[0] + h3 * s4 + h4 * s3;
-  d[3] += h0 * r.l[3] + h1 * r.l[2] + h2 * r.l[1] + h3 * r.l[0] + h4 * s4;
-  d[4] += h0 * r.l[4] + h1 * r.l[3] + h2 * r.l[2] + h3 * r.l[1] + h4 * r.l[0];
-}
-
-// Column sums -> limbs (< 2^26, limb 1 < 2^26 + 2^8). The top carry times 5 is formed in 64 bits: with
-// up to four products summed (p_sop4) the carry out of column 4 reaches 2^31.
-__device__ __forceinline__ P130 p_red(uint64_t (&d)[5]) {
-  P130 o;
-  uint64_t c;
-  c = d[0] >> 26; o.l[0] = (uint32_t)d[0] & M26; d[1] += c;
-  c = d[1] >> 26; o.l[1] = (uint32_t)d[1] & M26; d[2] += c;
-  c = d[2] >> 26; o.l[2] = (uint32_t)d[2] & M26; d[3] += c;
-  c = d[3] >> 26; o.l[3] = (uint32_t)d[3] & M26; d[4] += c;
-  c = d[4] >> 26; o.l[4] = (uint32_t)d[4] & M26;
-  const uint64_t t = c * 5u + o.l[0];
-  o.l[0] = (uint32_t)t & M26;
-  o.l[1] += (uint32_t)(t >> 26);
-  return o;
-}
-
-// h * r mod p, partially reduced (limbs < 2^26 + small). Inputs: limbs < 2^27.
-__device__ __forceinline__ P130 p_mul(const P130& h, const P130& r) {
-  uint64_t d[5] = {0, 0, 0, 0, 0};
-  p_mac(d, h, r);
-  return p_red(d);
-}
-
-// Add a full 16-byte block (raw LE words) plus 2^128 (poly1305.rs:39-43).
-__device__ __forceinline__ void p_add_block(P130& h, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
-  h.l[0] += w0 & M26;
-  h.l[1] += ((w0 >> 26) | (w1 << 6)) & M26;
-  h.l[2] += ((w1 >> 20) | (w2 << 12)) & M26;
-  h.l[3] += ((w2 >> 14) | (w3 << 18)) & M26;
-  h.l[4] += (w3 >> 8) | (1u << 24);
-}
-
-__device__ __forceinline__ void p_add(P130& a, const P130& b) { for (int i = 0; i < 5; i++) a.l[i] += b.l[i]; }
-
-// A full data slot's MAC in one reduction (SOP): acc' = acc r^(4G) + c0 r^3 + c1 r^2 + c2 r + c3, the
-// four products summed as 64-bit column sums before one carry chain, instead of three Horner steps and
-// the slot step, each reduced (four carry chains). Column sums stay below 2^59 (p_red). The acc product
-// goes last so the data words die as they are folded. Same-box A/B over 3 rounds
-// (profiles/r03/ab_c3_w2.log): C3 seal kernel 0.0878 -> 0.0840 ms; with the acc product first it spilled
-// 19 VGPRs and measured 12 % slower (profiles/r03/ab_c3_sop_rot16.log).
-__device__ __forceinline__ void p_sop4(P130& acc, bool first, const P130& rG, const uint32_t (&X)[16],
-                                       const P130& r, const P130& rsq, const P130& rcu) {
-  uint64_t d[5];
-  P130 c = p_zero();
-  p_add_block(c, X[12], X[13], X[14], X[15]);
-  for (int i = 0; i < 5; i++) d[i] = c.l[i];
-  c = p_zero();
-  p_add_block(c, X[0], X[1], X[2], X[3]);
-  p_mac(d, c, rcu);
-  c = p_zero();
-  p_add_block(c, X[4], X[5], X[6], X[7]);
-  p_mac(d, c, rsq);
-  c = p_zero();
-  p_add_block(c, X[8], X[9], X[10], X[11]);
-  p_mac(d, c, r);
-  if (!first) p_mac(d, acc, rG);
-  acc = p_red(d);
-}
-
-__device__ __forceinline__ void p_carry(P130& h) {
-  uint32_t c;
-  c = h.l[0] >> 26; h.l[0] &= M26; h.l[1] += c;
-  c = h.l[1] >> 26; h.l[1] &= M26; h.l[2] += c;
-  c = h.l[2] >> 26; h.l[2] &= M26; h.l[3] += c;
-  c = h.l[3] >> 26; h.l[3] &= M26; h.l[4] += c;
-  c = h.l[4] >> 26; h.l[4] &= M26; h.l[0] += c * 5;
-  c = h.l[0] >> 26; h.l[0] &= M26; h.l[1] += c;
-}
-
-// tag = ((h mod p) + s) mod 2^128 as raw words (poly1305.rs:46-50).
-__device__ __forceinline__ void p_finish(P130 h, const uint32_t s[4], uint32_t t[4]) {
-  p_carry(h);
-  p_carry(h);
-  uint32_t g0 = h.l[0] + 5, c = g0 >> 26; g0 &= M26;
-  uint32_t g1 = h.l[1] + c; c = g1 >> 26; g1 &= M26;
-  uint32_t g2 = h.l[2] + c; c = g2 >> 26; g2 &= M26;
-  uint32_t g3 = h.l[3] + c; c = g3 >> 26; g3 &= M26;
-  uint32_t g4 = h.l[4] + c - (1u << 26);
-  uint32_t mask = (g4 >> 31) - 1u;  // all ones if h >= p
-  uint32_t h0 = (h.l[0] & ~mask) | (g0 & mask), h1 = (h.l[1] & ~mask) | (g1 & mask);
-  uint32_t h2 = (h.l[2] & ~mask) | (g2 & mask), h3 = (h.l[3] & ~mask) | (g3 & mask);
-  uint32_t h4 = (h.l[4] & ~mask) | (g4 & mask);
-  uint32_t w0 = h0 | (h1 << 26), w1 = (h1 >> 6) | (h2 << 20), w2 = (h2 >> 12) | (h3 << 14), w3 = (h3 >> 18) | (h4 << 8);
-  uint64_t f = (uint64_t)w0 + s[0]; t[0] = (uint32_t)f;
-  f = (uint64_t)w1 + s[1] + (f >> 32); t[1] = (uint32_t)f;
-  f = (uint64_t)w2 + s[2] + (f >> 32); t[2] = (uint32_t)f;
-  f = (uint64_t)w3 + s[3] + (f >> 32); t[3] = (uint32_t)f;
-}
-
-template <int G>
-__device__ __forceinline__ P130 shfl_p(const P130& v, int src) {
-  P130 o;
-  for (int i = 0; i < 5; i++) o.l[i] = __shfl(v.l[i], src, G);
-  return o;
-}
-
 // ---- ChaCha20 block (chacha20/cipher.rs:56-87) ----
 #define QR(a, b, c, d)                      \
   a += b; d = rotl32(d ^ a, 16);            \
@@ -988,181 +876,6 @@ __global__ __launch_bounds__(kChSingleThreads) void chacha_single(ChSingle) {
   if (threadIdx.x == 0) __hip_atomic_store(A.done, A.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// ---- The single call at four lanes per ChaCha20 block (round 5) ----------------------------
-// chacha_single (64 lanes) runs a record's ChaCha20 blocks one per lane -- a 1,537-B record's 26 blocks each
-// ~1,300 VALU slots deep on one lane, the four columns as instruction-level parallelism of one wave -- and its
-// Poly1305 pieces four per lane (slot Horner, r-power scan, lane combine). Here a 4-wave workgroup gives each
-// block a quad of lanes, one state column per lane (the diagonal round takes its b, c, d words from the
-// quad's other lanes by DPP quad_perm and hands them back after), so the keystream is ~300 dependent slots
-// deep; and each Poly1305 message block gets a thread of its own: thread t holds block t of
-// AAD || pad || ciphertext || pad || lengths (poly1305.rs:57-66) and adds m_t r^(Q-t) (the Horner sum
-// a = sum m_t r^(Q-t), poly1305.rs:32-45), r^k read from entry k-1 of a 256-thread prefix-product scan.
-// Records whose argument block fits (kSingleInline): at most 56 data blocks + the key block (64 quads) and
-// Q <= 226 message blocks (256 threads).
-#ifndef ATLS_CHACHA_SINGLE_Q4
-#define ATLS_CHACHA_SINGLE_Q4 1
-#endif
-template <int CTRL>
-__device__ __forceinline__ uint32_t qperm(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);  // quad_perm
-}
-#define QRL(a, b, c, d)                     \
-  a += b; d = rotl32(d ^ a, 16);            \
-  c += d; b = rotl32(b ^ c, 12);            \
-  a += b; d = rotl32(d ^ a, 8);             \
-  c += d; b = rotl32(b ^ c, 7);
-
-// One RAW record (the Cipher-trait call) by the 256 threads of the workgroup: k its key slot, bytes the
-// base d.aux_off / d.in_off index (IV || AAD || input; the received tag at bytes + tag_off on open), outputs
-// at out + d.out_off, the tag at tag_out, the open result at *res. The caller releases the stores.
-template <bool OPEN>
-__device__ __forceinline__ void q4_record(const KeySched* k, const atls_rec& d, const uint8_t* bytes, uint32_t tag_off,
-                                          uint8_t* out, uint8_t* tag_out, atls_open_result* res) {
-  const int t = (int)threadIdx.x, q = t & 3, lane = t & 63, wv = t >> 6;
-  const uint32_t blk = (uint32_t)t >> 2;  // ChaCha20 block counter of this quad (0 = Poly1305 key)
-  __shared__ uint32_t ctw[64 * 16];        // MAC input words (ciphertext, zero past the end)
-  __shared__ uint32_t pw[256][5];          // r^(k+1) at k
-  __shared__ uint32_t rs[8];               // r, s (poly1305.rs:19-26)
-  __shared__ uint32_t part[4][5];
-  const uint32_t n = d.len, aad_len = d.aad_len;
-  const uint8_t* iv = bytes + d.aux_off;
-  const uint8_t* aadp = iv + 12;
-  const uint8_t* src = bytes + d.in_off;
-  uint8_t* dst = out + d.out_off;
-  const uint32_t na = (aad_len + 15u) / 16u, nct = (n + 15u) / 16u, jmax = (n + 63u) / 64u;
-  const uint32_t Q = na + nct + 1u;
-  // ---- keystream: column q of block blk (cipher.rs:56-87), every quad (those past jmax idle after) ----
-  const uint32_t kq = k->kw[q], kq4 = k->kw[4 + q];
-  const uint32_t nq = q ? ((uint32_t)iv[4 * q - 4] | ((uint32_t)iv[4 * q - 3] << 8) | ((uint32_t)iv[4 * q - 2] << 16) |
-                           ((uint32_t)iv[4 * q - 1] << 24))
-                        : blk;
-  const uint32_t c0 = q == 0 ? 0x61707865u : q == 1 ? 0x3320646eu : q == 2 ? 0x79622d32u : 0x6b206574u;
-  uint32_t a = c0, b = kq, c = kq4, dd = nq;
-#pragma unroll
-  for (int i = 0; i < 10; i++) {
-    QRL(a, b, c, dd)
-    b = qperm<0x39>(b); c = qperm<0x4E>(c); dd = qperm<0x93>(dd);  // diagonal: columns q+1, q+2, q+3
-    QRL(a, b, c, dd)
-    b = qperm<0x93>(b); c = qperm<0x4E>(c); dd = qperm<0x39>(dd);  // back to column q
-  }
-  const uint32_t o[4] = {a + c0, b + kq, c + kq4, dd + nq};  // words q, 4 + q, 8 + q, 12 + q of the block
-  if (blk == 0 && t < 4) {
-    rs[q] = o[0];
-    rs[4 + q] = o[1];
-  }
-  // ---- XOR, store, MAC words: word 4 kk + q of data block blk (bytes 64 (blk - 1) ..) ----
-  if (blk >= 1 && blk <= jmax) {
-    const uint32_t off = 64u * (blk - 1u), vb = min(64u, n - off);
-    const bool skip_xor = (n % 64u) == 0u && blk == jmax;  // cipher.rs:99-102
-#pragma unroll
-    for (int kk = 0; kk < 4; kk++) {
-      const uint32_t p0 = 16u * kk + 4u * (uint32_t)q;
-      uint32_t in = 0;
-      if (p0 + 4u <= vb) in = ld4(src + off + p0);
-      else
-        for (uint32_t x = 0; x < 4u; x++)
-          if (p0 + x < vb) in |= (uint32_t)src[off + p0 + x] << (8 * x);
-      uint32_t ct = skip_xor ? in : in ^ o[kk];
-      if (p0 + 4u > vb) ct &= p0 >= vb ? 0u : (0xffffffffu >> (8 * (p0 + 4u - vb)));
-      if (p0 + 4u <= vb) st4(dst + off + p0, ct);
-      else
-        for (uint32_t x = 0; x < 4u; x++)
-          if (p0 + x < vb) dst[off + p0 + x] = (uint8_t)(ct >> (8 * x));
-      ctw[16u * (blk - 1u) + 4u * kk + (uint32_t)q] = OPEN ? in : ct;  // the MAC runs over the ciphertext
-    }
-  }
-  __syncthreads();
-  // ---- r powers: thread t holds r^(t+1) (prefix products, 6 levels per wave, then the wave's (r^64)^w) ----
-  const uint32_t r0 = rs[0] & 0x0fffffffu, r1 = rs[1] & 0x0ffffffcu, r2 = rs[2] & 0x0ffffffcu, r3 = rs[3] & 0x0ffffffcu;
-  const uint32_t sk[4] = {rs[4], rs[5], rs[6], rs[7]};
-  P130 r;
-  r.l[0] = r0 & M26;
-  r.l[1] = ((r0 >> 26) | (r1 << 6)) & M26;
-  r.l[2] = ((r1 >> 20) | (r2 << 12)) & M26;
-  r.l[3] = ((r2 >> 14) | (r3 << 18)) & M26;
-  r.l[4] = r3 >> 8;
-  P130 R = r;
-#pragma unroll
-  for (int dl = 1; dl < 64; dl <<= 1) {
-    if ((uint32_t)dl < Q) {  // uniform: powers past r^Q are not read
-      P130 u;
-#pragma unroll
-      for (int i = 0; i < 5; i++) u.l[i] = __shfl_up(R.l[i], (unsigned)dl, 64);
-      const P130 m = p_mul(R, u);
-      if (lane >= dl) R = m;
-    }
-  }
-  if (wv >= 1 && Q > 64u * (uint32_t)wv) {  // this wave's entries are r^(64 w + lane + 1)
-    const P130 r64 = shfl_p<64>(R, 63);
-    P130 f = r64;
-    if (wv >= 2) {
-      const P130 f2 = p_mul(r64, r64);
-      f = wv == 2 ? f2 : p_mul(f2, r64);
-    }
-    R = p_mul(R, f);
-  }
-#pragma unroll
-  for (int i = 0; i < 5; i++) pw[t][i] = R.l[i];
-  __syncthreads();
-  // ---- message block t times r^(Q - t), summed ----
-  P130 h = p_zero();
-  if ((uint32_t)t < Q) {
-    uint32_t w[4] = {0, 0, 0, 0};
-    if ((uint32_t)t < na) {
-#pragma unroll
-      for (int x = 0; x < 16; x++)
-        if (16u * (uint32_t)t + (uint32_t)x < aad_len) w[x >> 2] |= (uint32_t)aadp[16 * t + x] << (8 * (x & 3));
-    } else if ((uint32_t)t < na + nct) {
-      const uint32_t pc = (uint32_t)t - na;
-#pragma unroll
-      for (int x = 0; x < 4; x++) w[x] = ctw[4u * pc + (uint32_t)x];
-    } else {  // le64(aad_len) || le64(ct_len) (poly1305.rs:63-64)
-      w[0] = aad_len;
-      w[2] = n;
-    }
-    P130 m = p_zero();
-    p_add_block(m, w[0], w[1], w[2], w[3]);
-    const uint32_t e = Q - (uint32_t)t;  // 1 .. Q
-    P130 pe;
-#pragma unroll
-    for (int i = 0; i < 5; i++) pe.l[i] = pw[e - 1u][i];
-    h = p_mul(m, pe);
-  }
-  for (int off = 32; off >= 1; off >>= 1) {
-    if (off == 1) p_carry(h);  // 32 partials summed: limbs < 2^31; carried before the last doubling
-    P130 u;
-#pragma unroll
-    for (int i = 0; i < 5; i++) u.l[i] = __shfl_xor(h.l[i], off, 64);
-    p_add(h, u);
-  }
-  if (lane == 0) {
-    p_carry(h);
-#pragma unroll
-    for (int i = 0; i < 5; i++) part[wv][i] = h.l[i];
-  }
-  __syncthreads();
-  if (t == 0) {
-#pragma unroll
-    for (int x = 1; x < 4; x++)
-#pragma unroll
-      for (int i = 0; i < 5; i++) h.l[i] += part[x][i];
-    uint32_t tag[4];
-    p_finish(h, sk, tag);
-    if (!OPEN) {
-      st16(tag_out, make_uint4(tag[0], tag[1], tag[2], tag[3]));
-    } else {
-      const uint4 tg = ld16(bytes + tag_off);
-      const bool ok = (tg.x == tag[0]) & (tg.y == tag[1]) & (tg.z == tag[2]) & (tg.w == tag[3]);
-      atls_open_result rr;
-      rr.reserved[0] = rr.reserved[1] = 0;
-      rr.status = ok ? ATLS_OK : ATLS_BAD_RECORD_MAC;  // RAW: Cipher::decrypt (poly1305.rs:91-96)
-      rr.content_len = n;
-      rr.content_type = 0;
-      *res = rr;
-    }
-  }
-}
-#undef QRL
 
 // q4_record with the record's bytes and its output passing through LDS in 16-byte pieces: its 4-byte and byte
 // accesses straight to mapped host memory would each be a PCIe transaction (the resident server's request and
@@ -1172,13 +885,14 @@ template <bool OPEN>
 __device__ __forceinline__ void q4_staged(const KeySched* k, const atls_rec& d, const uint8_t* in, uint32_t tag_off,
                                           uint8_t* out, uint8_t* tag_out, atls_open_result* res) {
   __shared__ uint4 stage_in[kSingleInline / 16], stage_out[kSingleInline / 16];
+  __shared__ Q4Lds q4l;
   const uint32_t t = threadIdx.x;
   const uint32_t nin = (tag_off + (OPEN ? 16u : 0u) + 15u) / 16u, nout = (d.len + 15u) / 16u;  // <= 224 each
   for (uint32_t i = t; i < nin; i += 256u) stage_in[i] = ld16(in + 16u * i);
   __syncthreads();
   atls_rec dl = d;
   dl.out_off = 0;
-  q4_record<OPEN>(k, dl, (const uint8_t*)stage_in, tag_off, (uint8_t*)stage_out, tag_out, res);
+  q4_record<OPEN>(k, dl, (const uint8_t*)stage_in, tag_off, (uint8_t*)stage_out, tag_out, res, q4l);
   __syncthreads();  // the output is whole in LDS
   for (uint32_t i = t; i < nout; i += 256u) st16(out + d.out_off + 16u * i, stage_out[i]);
 }
@@ -1194,106 +908,6 @@ __global__ __launch_bounds__(256) void chacha_single_q4(ChSingle) {
   if (threadIdx.x == 0) __hip_atomic_store(A.done, A.done_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// ---- The resident single-call server (opt-in, ATLS_SINGLE_RESIDENT=1) ----------------------
-// A launch costs 5.9-6.4 us before the first instruction and after the flag (tools/single_call_floor.hip:
-// empty_launch_*_flag_spin_us); a wave that stays resident and polls a doorbell word in mapped host memory
-// answers in 1.7 us, 4.2 us with 1,552 B read from and written to mapped memory (resident_wave_doorbell_*).
-// chacha_resident is one workgroup serving every call context of the process (a resident kernel holds its
-// hardware queue, and the process has few: one server, not one per context). The mapped block has a slot per
-// context (doorbell, flag, request, reply) and a common area (alive, stop). Lanes 0..7 of wave 0 poll the
-// slots' doorbells and flags (s_sleep between polls; the other waves wait at the barrier); a slot whose
-// doorbell differs from the value last served there holds request v = the doorbell value: its header and the
-// largest request a slot holds come into LDS in one round trip of 16-byte loads, q4_record seals / opens it
-// from LDS into LDS, the reply goes out in 16-byte stores, then the slot's flag := v. The server
-// leaves on the stop word or after idle_us without a request, writing alive := 0 as its last store -- an
-// exit every wave reaches whatever the host does (the host sets the stop word at exit).
-struct ResidentReq {
-  const KeySched* ks;  // the key slot's schedule (device memory)
-  atls_rec d;          // in_off / aux_off index bytes; out_off indexes the reply area
-  uint32_t tag_off;
-  uint32_t open;
-};
-constexpr int kResSlots = 8;
-constexpr size_t kResBell = 0, kResFlag = 64, kResReq = 256, kResTag = 512, kResRes = 528, kResBytes = 1024,
-                 kResOut = 8192, kResSlotBytes = 16384, kResCommon = kResSlots * kResSlotBytes, kResAlive = kResCommon,
-                 kResStopAt = kResCommon + 64;
-static_assert(kResBytes + kSingleInline <= kResOut && kResOut + kSingleInline + 16 <= kResSlotBytes, "resident slot");
-
-__global__ __launch_bounds__(256) void chacha_resident(uint8_t* blk, uint32_t idle_us) {
-  __shared__ int cmd_slot;
-  __shared__ uint32_t cmd_v;
-  __shared__ uint4 hdr[4];  // the request (ResidentReq, 64 B)
-  __shared__ uint4 stage_in[kSingleInline / 16], stage_out[kSingleInline / 16];
-  static_assert(sizeof(ResidentReq) == sizeof(hdr), "request header");
-  const int t = (int)threadIdx.x;
-  // lane i < 8 of wave 0 keeps the last value it served for slot i (the flag the host set before this server)
-  uint32_t served = 0;
-  if (t < kResSlots)
-    served = __hip_atomic_load((uint32_t*)(blk + (size_t)t * kResSlotBytes + kResFlag), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-  for (;;) {
-    if (t < 64) {  // wave 0: lanes 0..7 watch the slots' doorbells (one uncached load per lane and poll)
-      const uint32_t* bell = (const uint32_t*)(blk + (size_t)(t < kResSlots ? t : 0) * kResSlotBytes + kResBell);
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      int slot = -1;
-      uint32_t v = 0;
-      for (uint32_t it = 0;; it++) {
-        const uint32_t b = t < kResSlots ? __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
-        const unsigned long long m = __ballot(t < kResSlots && b != 0u && b != served);
-        if (m) {
-          slot = __builtin_ffsll((long long)m) - 1;
-          v = (uint32_t)__shfl((int)b, slot, 64);
-          break;
-        }
-        if ((it & 15u) == 15u) {
-          const uint32_t stop = __builtin_amdgcn_readfirstlane(
-              __hip_atomic_load((uint32_t*)(blk + kResStopAt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-          if (stop || __builtin_amdgcn_s_memrealtime() - t0 > 100ull * idle_us) break;  // told to stop, or idle
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (t == 0) {
-        cmd_slot = slot;
-        cmd_v = v;
-      }
-      if (slot >= 0 && t == slot) served = v;
-    }
-    __syncthreads();
-    const int slot = cmd_slot;
-    const uint32_t v = cmd_v;
-    if (slot < 0) break;
-    uint8_t* sl = blk + (size_t)slot * kResSlotBytes;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request the host wrote before the doorbell
-    // header and every byte a request can hold, in one round trip (the request's own size is in the header)
-    if (t < (int)(kSingleInline / 16)) stage_in[t] = ((const uint4*)(sl + kResBytes))[t];
-    else if (t < (int)(kSingleInline / 16) + 4) hdr[t - kSingleInline / 16] = ((const uint4*)(sl + kResReq))[t - kSingleInline / 16];
-    __syncthreads();  // (also: every wave has read the command before wave 0 may overwrite it)
-    ResidentReq R;
-    __builtin_memcpy(&R, hdr, sizeof R);
-    atls_rec dl = R.d;
-    dl.out_off = 0;
-    if (R.open)
-      q4_record<true>(R.ks, dl, (const uint8_t*)stage_in, R.tag_off, (uint8_t*)stage_out, sl + kResTag,
-                      (atls_open_result*)(sl + kResRes));
-    else
-      q4_record<false>(R.ks, dl, (const uint8_t*)stage_in, R.tag_off, (uint8_t*)stage_out, sl + kResTag,
-                       (atls_open_result*)(sl + kResRes));
-    __syncthreads();  // the reply is whole in LDS
-    const uint32_t nout = (R.d.len + 15u) / 16u;
-    for (uint32_t i = (uint32_t)t; i < nout; i += 256u) ((uint4*)(sl + kResOut))[i] = stage_out[i];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // every wave's stores have left
-    if (t == 0) __hip_atomic_store((uint32_t*)(sl + kResFlag), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    __hip_atomic_store((uint32_t*)(blk + kResAlive), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
-// The single call's records that do not fit the argument block (descriptor and data in the pinned block),
-// on the same 4-wave record.
 template <bool OPEN>
 __global__ __launch_bounds__(256) void chacha_single_ptr(ChArgs A) {
   const WorkList W{nullptr, nullptr, kListChacha, 1u};
@@ -1354,11 +968,6 @@ extern "C" int atls_launch_chacha_single(int open, const void* ks, uint32_t n_sl
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
 
-// The resident single-call server on stream s (chacha_resident): blk = the mapped block's device address.
-extern "C" int atls_launch_chacha_resident(uint8_t* blk, uint32_t idle_us, hipStream_t s) {
-  hipLaunchKernelGGL(atls::chacha_resident, dim3(1), dim3(256), 0, s, blk, idle_us);
-  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
-}
 
 // idx / plan: the batch plan's work lists (G = 16), or nullptr for a direct batch (per-step widths).
 extern "C" int atls_launch_chacha(int open, const void* ks, const atls_rec* recs, uint32_t n, const uint8_t* in,

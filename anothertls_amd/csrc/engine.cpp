@@ -42,7 +42,7 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
                                const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
 extern "C" size_t atls_group_hdr_offset(uint32_t n_slots);
-extern "C" int atls_launch_chacha_resident(uint8_t* blk, uint32_t idle_us, hipStream_t s);
+extern "C" int atls_launch_single_resident(uint8_t* blk, uint32_t idle_us, int gcm, hipStream_t s);
 extern "C" int atls_launch_clock_probe(uint32_t wgs, uint32_t delay_us, uint32_t spin_us, uint64_t* out, hipStream_t s);
 extern "C" int atls_launch_sync_flag(const uint32_t* err, uint32_t* out, uint32_t val, hipStream_t s);
 extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t n_slots, const atls_rec* d,
@@ -833,13 +833,17 @@ int cached_slot(SingleCtx* c, uint16_t suite, const uint8_t* key, size_t key_len
 }
 
 // ---- the resident single-call server (opt-in) ----
-bool resident_enabled() {
-  static const bool v = [] {
+// ATLS_SINGLE_RESIDENT: 1 = ChaCha20-Poly1305 calls through the server, 2 = AES-GCM calls too (the server with
+// the AES-GCM path serves ChaCha20-Poly1305 0.9 us slower: profiles/r05/single/ab_resident_gcm.log)
+int resident_mode() {
+  static const int v = [] {
     const char* e = std::getenv("ATLS_SINGLE_RESIDENT");
-    return e && std::atoi(e) != 0;
+    const int m = e ? std::atoi(e) : 0;
+    return m == 1 || m == 2 ? m : 0;
   }();
   return v;
 }
+bool resident_enabled() { return resident_mode() != 0; }
 uint32_t resident_idle_us() {  // ATLS_SINGLE_RESIDENT_IDLE_MS: how long a server waits for the next call (20 ms)
   static const uint32_t v = [] {
     const char* e = std::getenv("ATLS_SINGLE_RESIDENT_IDLE_MS");
@@ -848,20 +852,25 @@ uint32_t resident_idle_us() {  // ATLS_SINGLE_RESIDENT_IDLE_MS: how long a serve
   }();
   return v;
 }
-// The process's resident ChaCha20-Poly1305 single-call server (ATLS_SINGLE_RESIDENT=1, chacha.hip
-// chacha_resident): one mapped, coherent block with a slot per call context (doorbell, flag, request, reply)
+// The process's resident single-call server for both suites (ATLS_SINGLE_RESIDENT=1, gcm.hip single_resident): one mapped, coherent block with a slot per call context (doorbell, flag, request, reply)
 // and a common area (alive, stop), one stream, one workgroup -- a resident kernel holds a hardware queue,
 // so there is one server for the whole process, not one per context.
 constexpr int kResSlots = 8;
 constexpr size_t kResBell = 0, kResFlag = 64, kResReq = 256, kResTag = 512, kResRes = 528, kResBytes = 1024,
                  kResOut = 8192, kResSlotBytes = 16384, kResCommon = kResSlots * kResSlotBytes, kResAlive = kResCommon,
                  kResStopAt = kResCommon + 64, kResBlock = kResCommon + 4096;
-struct ResidentReqH {  // chacha.hip ResidentReq
+struct ResidentReqH {  // gcm.hip ResidentReq
   const void* ks;
   atls_rec d;
   uint32_t tag_off;
   uint32_t open;
+  uint32_t nr;  // 0: ChaCha20-Poly1305; 10 / 12 / 14: AES-GCM
+  uint32_t pad0;
+  const void* t0;
+  void* err;
+  uint64_t pad1[5];
 };
+static_assert(sizeof(ResidentReqH) == 128, "gcm.hip ResidentReq");
 struct ResidentServer {
   std::mutex mu;
   uint8_t* h = nullptr;
@@ -942,16 +951,16 @@ void resident_yield() {
 int resident_launch_locked(ResidentServer& S) {
   if (__atomic_load_n((uint32_t*)(S.h + kResAlive), __ATOMIC_SEQ_CST) != 0) return ATLS_OK;
   __atomic_store_n((uint32_t*)(S.h + kResAlive), 1u, __ATOMIC_SEQ_CST);
-  return atls_launch_chacha_resident(S.d, resident_idle_us(), S.s);
+  return atls_launch_single_resident(S.d, resident_idle_us(), resident_mode() == 2 ? 1 : 0, S.s);
 }
 
 // One call through the server: request into the context's slot, doorbell, then the slot's flag. Returns
 // ATLS_OK (outputs in the slot) or ATLS_INTERNAL_ERROR.
 int resident_call(SingleCtx* c, const void* ks, const atls_rec& d, const uint8_t* bytes, uint32_t nbytes, uint32_t tag_off,
-                  bool open) {
+                  bool open, uint32_t nr, const void* t0tab, void* err) {
   ResidentServer& S = resident_server();
   uint8_t* h = S.h + (size_t)c->res_slot * kResSlotBytes;
-  const ResidentReqH q{ks, d, tag_off, open ? 1u : 0u};
+  const ResidentReqH q{ks, d, tag_off, open ? 1u : 0u, nr, 0u, t0tab, err, {0, 0, 0, 0, 0}};
   std::memcpy(h + kResReq, &q, sizeof q);
   std::memcpy(h + kResBytes, bytes, nbytes);
   uint32_t v = ++c->res_seq;
@@ -1080,7 +1089,8 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
   hipStream_t s = e->stream;
-  if (inl && suite == ATLS_TLS_CHACHA20_POLY1305_SHA256 && resident_enabled() && resident_slot(c, e) >= 0) {
+  if (inl && resident_enabled() && (suite == ATLS_TLS_CHACHA20_POLY1305_SHA256 || resident_mode() == 2) &&
+      resident_slot(c, e) >= 0) {
     // the resident server: no launch per call (the new key's setup, if any, finishes first)
     if (installed && hipStreamSynchronize(s) != hipSuccess) return ATLS_INTERNAL_ERROR;
     uint8_t bytes[atls::kSingleInline];
@@ -1095,8 +1105,9 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
     uint8_t* rh = resident_server().h + (size_t)c->res_slot * kResSlotBytes;
     if (open) std::memset(rh + kResRes, 0xff, sizeof(atls_open_result));  // the server writes every field
     else std::memcpy(rh + kResTag, kTagCanary, 16);
+    const bool chacha = suite == ATLS_TLS_CHACHA20_POLY1305_SHA256;
     rc = resident_call(c, (const atls::KeySched*)e->ks.p + slot, d, bytes, (uint32_t)(inl_tag + (open ? 16 : 0)),
-                       (uint32_t)inl_tag, open);
+                       (uint32_t)inl_tag, open, chacha ? 0u : (uint32_t)key_len / 4u + 6u, e->t0.p, e->err.p);
     if (rc) return rc;
     if (!open) {
       if (std::memcmp(rh + kResTag, kTagCanary, 16) == 0) return ATLS_ILLEGAL_PARAMETER;

@@ -29,6 +29,7 @@
 #include <cstdlib>
 
 #include "gcm_common.h"
+#include "chacha_q4.h"
 
 namespace atls {
 
@@ -1289,6 +1290,175 @@ __global__ __launch_bounds__(64 * kSingleWaves) void gcm_single_ptr(GcmArgs A) {
   single_record<OPEN, NR>(A);
 }
 
+// ---- The resident single-call server (opt-in, ATLS_SINGLE_RESIDENT=1) ----------------------
+// A launch costs 5.9-6.4 us before the first instruction and after the flag (tools/single_call_floor.hip:
+// empty_launch_*_flag_spin_us); a wave that stays resident and polls a doorbell word in mapped host memory
+// answers in 1.7 us, 4.2 us with 1,552 B read from and written to mapped memory (resident_wave_doorbell_*).
+// single_resident is one workgroup serving every call context of the process, both suites (a resident kernel
+// holds its hardware queue, and the process has few: one server, not one per context or suite). The mapped
+// block has a slot per context (doorbell, flag, request, reply) and a common area (alive, stop). Lanes 0..7 of
+// wave 0 poll the slots' doorbells (s_sleep between polls; the other waves wait at the barrier); a slot whose
+// doorbell differs from the value last served there holds request v = the doorbell value: its header and the
+// largest request a slot holds come into LDS in one round trip of 16-byte loads, the record is sealed / opened
+// from LDS into LDS -- ChaCha20-Poly1305 by q4_record (chacha_q4.h), AES-GCM by the single call's 4-wave
+// gcm_record over the T-tables this server built once, when its first AES-GCM request came -- the reply goes
+// out in 16-byte stores, then the slot's flag := v. The server leaves on the stop word or after idle_us
+// without a request, writing alive := 0 as its last store -- an exit every wave reaches whatever the host does
+// (the host sets the stop word at exit).
+struct ResidentReq {
+  const KeySched* ks;   // the key slot's schedule (device memory)
+  atls_rec d;           // in_off / aux_off index bytes, key_slot 0 (ks is the slot's), out_off indexes the reply
+  uint32_t tag_off;     // open: the received tag at bytes + tag_off
+  uint32_t open;
+  uint32_t nr;          // 0: ChaCha20-Poly1305; 10 / 12 / 14: AES-GCM with that many rounds
+  uint32_t pad0;
+  const uint32_t* t0;   // AES-GCM: the 256-entry T-table (global memory) the LDS tables are built from
+  uint32_t* err;        // AES-GCM: the engine's sticky error word (the descriptor check's)
+  uint64_t pad1[5];
+};
+static_assert(sizeof(ResidentReq) == 128, "resident request header");
+constexpr int kResSlots = 8;
+constexpr size_t kResBell = 0, kResFlag = 64, kResReq = 256, kResTag = 512, kResRes = 528, kResBytes = 1024,
+                 kResOut = 8192, kResSlotBytes = 16384, kResCommon = kResSlots * kResSlotBytes, kResAlive = kResCommon,
+                 kResStopAt = kResCommon + 64;
+static_assert(kResReq + sizeof(ResidentReq) <= kResTag, "resident request header");
+static_assert(kResBytes + kSingleInline <= kResOut && kResOut + kSingleInline + 16 <= kResSlotBytes, "resident slot");
+
+template <int NR, bool OPEN>
+__device__ __forceinline__ void resident_gcm(const ResidentReq& R, const atls_rec* rec, const uint8_t* in, uint8_t* out,
+                                             uint8_t* sl) {
+  const GcmArgs A{R.ks, rec, 1u, in, in, out, sl + kResTag, in + R.tag_off, (atls_open_result*)(sl + kResRes), R.t0,
+                  nullptr, nullptr, R.err, 1u, nullptr, nullptr, nullptr, 0u};
+  const int t = (int)threadIdx.x;
+  gcm_one<NR, OPEN, true, 64 * kSingleWaves>(A, 0u, 4u * (uint32_t)(t & 31), (uint32_t)kTabBytes, t);
+}
+
+// The server's LDS past the AES-GCM area: the server has no static LDS, so the T-tables the GCM code addresses
+// absolutely (TA: byte value << 8 | lane) sit at LDS address 0 as in the single-call kernels.
+struct ResidentLds {
+  uint4 stage_in[kSingleInline / 16], stage_out[kSingleInline / 16];
+  uint4 hdr[sizeof(ResidentReq) / 16];
+  atls_rec rec;
+  int cmd_slot;
+  uint32_t cmd_v;
+  uint32_t pad[2];
+  Q4Lds q4;
+};
+constexpr size_t kResidentLds = kSingleLds + sizeof(ResidentLds);
+static_assert(kSingleLds % 16 == 0 && kResidentLds <= 160u * 1024u, "the resident server's LDS");
+
+// GCM = false: a ChaCha20-Poly1305-only server (ATLS_SINGLE_RESIDENT=1). The server with the AES-GCM path takes
+// 217 VGPRs against 100, and its ChaCha20-Poly1305 calls measured 0.9 us slower with the keystream code
+// unchanged (profiles/r05/single/ab_resident_gcm.log), so both suites on one server is its own mode (=2).
+template <bool GCM>
+__global__ __launch_bounds__(64 * kSingleWaves) void single_resident(uint8_t* blk, uint32_t idle_us) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // AES-GCM: T-tables, GHASH areas (kSingleLds)
+  ResidentLds& S = *reinterpret_cast<ResidentLds*>(smem + kSingleLds / 4);
+  int& cmd_slot = S.cmd_slot;
+  uint32_t& cmd_v = S.cmd_v;
+  uint4* hdr = S.hdr;
+  uint4* stage_in = S.stage_in;
+  uint4* stage_out = S.stage_out;
+  atls_rec& rec = S.rec;
+  const int t = (int)threadIdx.x;
+  bool tables = false;  // the AES T-tables are in LDS (built at this server's first AES-GCM request)
+  // lane i < 8 of wave 0 keeps the last value it served for slot i (the flag the host set before this server)
+  uint32_t served = 0;
+  if (t < kResSlots)
+    served = __hip_atomic_load((uint32_t*)(blk + (size_t)t * kResSlotBytes + kResFlag), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    if (t < 64) {  // wave 0: lanes 0..7 watch the slots' doorbells (one uncached load per lane and poll)
+      const uint32_t* bell = (const uint32_t*)(blk + (size_t)(t < kResSlots ? t : 0) * kResSlotBytes + kResBell);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      int slot = -1;
+      uint32_t v = 0;
+      for (uint32_t it = 0;; it++) {
+        const uint32_t b = t < kResSlots ? __hip_atomic_load(bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+        const unsigned long long m = __ballot(t < kResSlots && b != 0u && b != served);
+        if (m) {
+          slot = __builtin_ffsll((long long)m) - 1;
+          v = (uint32_t)__shfl((int)b, slot, 64);
+          break;
+        }
+        if ((it & 15u) == 15u) {
+          const uint32_t stop = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load((uint32_t*)(blk + kResStopAt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+          if (stop || __builtin_amdgcn_s_memrealtime() - t0 > 100ull * idle_us) break;  // told to stop, or idle
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (t == 0) {
+        cmd_slot = slot;
+        cmd_v = v;
+      }
+      if (slot >= 0 && t == slot) served = v;
+    }
+    __syncthreads();
+    const int slot = cmd_slot;
+    const uint32_t v = cmd_v;
+    if (slot < 0) break;
+    uint8_t* sl = blk + (size_t)slot * kResSlotBytes;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request the host wrote before the doorbell
+    // header and every byte a request can hold, in one round trip (the request's own size is in the header)
+    constexpr int kIn = (int)(kSingleInline / 16), kHdr = (int)(sizeof(ResidentReq) / 16);
+    if (t < kIn) stage_in[t] = ((const uint4*)(sl + kResBytes))[t];
+    else if (t < kIn + kHdr) hdr[t - kIn] = ((const uint4*)(sl + kResReq))[t - kIn];
+    __syncthreads();  // (also: every wave has read the command before wave 0 may overwrite it)
+    ResidentReq R;
+    __builtin_memcpy(&R, hdr, sizeof R);
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(R.nr), open = __builtin_amdgcn_readfirstlane(R.open);
+    atls_rec dl = R.d;
+    dl.out_off = 0;
+    if (nr == 0) {
+      if (open)
+        q4_record<true>(R.ks, dl, (const uint8_t*)stage_in, R.tag_off, (uint8_t*)stage_out, sl + kResTag,
+                        (atls_open_result*)(sl + kResRes), S.q4);
+      else
+        q4_record<false>(R.ks, dl, (const uint8_t*)stage_in, R.tag_off, (uint8_t*)stage_out, sl + kResTag,
+                         (atls_open_result*)(sl + kResRes), S.q4);
+    } else if constexpr (GCM) {
+      if (!tables) {  // T0 through the (still unused) GHASH area, then the replicated rows (single_record)
+        smem[kTabBytes / 4 + t] = R.t0[t];
+        __syncthreads();
+        for (int i = t; i < (int)(kTabBytes / 4); i += 64 * kSingleWaves) {
+          const uint32_t x = smem[kTabBytes / 4 + (i >> 6)];
+          smem[i] = (i & 32) ? rotl32(x, 8) : x;
+        }
+        tables = true;
+      }
+      if (t == 0) {
+        dl.key_slot = 0;
+        rec = dl;
+      }
+      __syncthreads();
+      const uint8_t* in = (const uint8_t*)stage_in;
+      uint8_t* out = (uint8_t*)stage_out;
+      if (nr == 10) {
+        if (open) resident_gcm<10, true>(R, &rec, in, out, sl);
+        else resident_gcm<10, false>(R, &rec, in, out, sl);
+      } else if (nr == 12) {
+        if (open) resident_gcm<12, true>(R, &rec, in, out, sl);
+        else resident_gcm<12, false>(R, &rec, in, out, sl);
+      } else {
+        if (open) resident_gcm<14, true>(R, &rec, in, out, sl);
+        else resident_gcm<14, false>(R, &rec, in, out, sl);
+      }
+    }
+    __syncthreads();  // the reply is whole in LDS
+    const uint32_t nout = (R.d.len + 15u) / 16u;
+    for (uint32_t i = (uint32_t)t; i < nout; i += 64u * kSingleWaves) ((uint4*)(sl + kResOut))[i] = stage_out[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's stores have left
+    if (t == 0) __hip_atomic_store((uint32_t*)(sl + kResFlag), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (t == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    __hip_atomic_store((uint32_t*)(blk + kResAlive), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace atls
 
 extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t n_slots, const atls_rec* d,
@@ -1415,4 +1585,13 @@ extern "C" int atls_debug_tt_stamps(unsigned long long* out) {
   (void)out;
   return -1;
 #endif
+}
+
+// The resident single-call server on stream s (single_resident): blk = the mapped block's device address; gcm:
+// the server also takes AES-GCM calls.
+extern "C" int atls_launch_single_resident(uint8_t* blk, uint32_t idle_us, int gcm, hipStream_t s) {
+  const dim3 b(64 * atls::kSingleWaves);
+  if (gcm) hipLaunchKernelGGL(atls::single_resident<true>, dim3(1), b, atls::kResidentLds, s, blk, idle_us);
+  else hipLaunchKernelGGL(atls::single_resident<false>, dim3(1), b, atls::kResidentLds, s, blk, idle_us);
+  return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }

@@ -1,7 +1,10 @@
 """Run by tests/test_gpu_single_resident.py in its own process (the mode is read once per process):
-ChaCha20-Poly1305 single calls through the resident server (ATLS_SINGLE_RESIDENT=1) against the oracle --
-lengths across the F4 quirk (chacha20/cipher.rs:99-102) and the argument-block limit, AADs of 0-40 bytes,
-seal / open / tampered tag, calls after the server left on its idle timeout, and 8 threads at once."""
+Cipher-trait single calls with the resident server on (ATLS_SINGLE_RESIDENT=1: ChaCha20-Poly1305 calls through
+it; =2: AES-GCM calls too, gcm.hip single_resident<true>) against the oracle: ChaCha20-Poly1305 at lengths across the F4 quirk
+(chacha20/cipher.rs:99-102) and the argument-block limit; AES-128/-192/-256-GCM (gcm.rs:42-162) with 12-byte
+and other IVs; AADs of 0-40 bytes; seal / open / tampered tag; suites interleaved; batch launches between
+calls (the server steps aside and comes back, building its AES tables again); calls after the server left on
+its idle timeout; and 8 threads at once."""
 import os
 import random
 import sys
@@ -11,18 +14,23 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 
+import numpy as np  # noqa: E402
+
 import anothertls_amd as atls  # noqa: E402
 import oracle as ora  # noqa: E402
 
+CHACHA, AES128, AES256 = 0x1303, 0x1301, 0x1302
 
-def one(c, rng, key, n, aad_len):
-    iv = bytes(rng.getrandbits(8) for _ in range(12))
+
+def one(ciphers, rng, suite, key, n, aad_len, iv_len=12):
+    c = ciphers[suite]
+    iv = bytes(rng.getrandbits(8) for _ in range(iv_len))
     aad = bytes(rng.getrandbits(8) for _ in range(aad_len))
     pt = bytes(rng.getrandbits(8) for _ in range(n))
     ct, tag = c.encrypt(key, iv, pt, aad)
-    rc, ect, etag = ora.cipher_encrypt(0x1303, key, iv, pt, aad)
-    assert rc == 0 and ct == ect and tag == etag, (n, aad_len)
-    assert c.decrypt(key, iv, ct, aad, tag) == pt
+    rc, ect, etag = ora.cipher_encrypt(suite, key, iv, pt, aad)
+    assert rc == 0 and ct == ect and tag == etag, (hex(suite), len(key), n, aad_len, iv_len)
+    assert c.decrypt(key, iv, ct, aad, tag) == pt, (hex(suite), n)
     try:
         c.decrypt(key, iv, ct, aad, tag[:7] + bytes([tag[7] ^ 2]) + tag[8:])
     except atls.TlsError as e:
@@ -31,28 +39,62 @@ def one(c, rng, key, n, aad_len):
         raise AssertionError("tampered tag accepted")
 
 
+def batch_launch():
+    """A batch on an engine of this process: the server must step aside (its hardware queue) and return."""
+    from anothertls_amd import workload
+    eng = atls.Engine(0)
+    b = workload.tls_batch(16, 1024, 0x1301, n_keys=4)
+    eng.set_keys(b["keys"])
+    h_in = np.random.default_rng(1).integers(0, 256, b["in_bytes"] + 16, dtype=np.uint8)
+    out, tags = np.zeros(b["out_bytes"] + 16, np.uint8), np.zeros(16 * 16, np.uint8)
+    eng.seal_batch(b["recs"], h_in, np.zeros(16, np.uint8), out, tags)
+    eng.close()
+
+
 def main():
-    assert os.environ.get("ATLS_SINGLE_RESIDENT") == "1"
+    assert os.environ.get("ATLS_SINGLE_RESIDENT") in ("1", "2")  # 2: AES-GCM calls through the server too
     rng = random.Random(0x5E5)
-    c = atls.CipherSuite(0x1303).get_cipher()
-    keys = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(3)]
-    print("first call", flush=True)
-    one(c, rng, keys[0], 1537, 5)
-    print("first call OK", flush=True)
+    ciphers = {s: atls.CipherSuite(s).get_cipher() for s in (CHACHA, AES128, AES256)}
+    keys = {CHACHA: [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(3)],
+            AES128: [bytes(rng.getrandbits(8) for _ in range(16)) for _ in range(3)],
+            AES256: [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(3)]}
+    print("first calls", flush=True)
+    one(ciphers, rng, CHACHA, keys[CHACHA][0], 1537, 5)
+    one(ciphers, rng, AES128, keys[AES128][0], 1537, 5)
+    print("first calls OK", flush=True)
+    lens = (0, 1, 15, 16, 17, 63, 64, 65, 127, 128, 1023, 1024, 1536, 1537, 3000, 3455, 3456, 3500, 3600, 16385)
     for aad_len in (0, 5, 40):
-        for n in (0, 1, 15, 16, 63, 64, 65, 127, 128, 1023, 1024, 1536, 1537, 3000, 3455, 3456, 3500, 3600, 16385):
-            one(c, rng, keys[n % 3], n, aad_len)
+        for n in lens:
+            one(ciphers, rng, CHACHA, keys[CHACHA][n % 3], n, aad_len)
+            one(ciphers, rng, AES128, keys[AES128][n % 3], n, aad_len)
+            one(ciphers, rng, AES256, keys[AES256][n % 3], n, aad_len)
         print("aad", aad_len, "OK", flush=True)
+    for iv_len in (1, 8, 16, 60):  # GCM's J0 from GHASH(IV) (gcm.rs:59-70)
+        for n in (0, 16, 1537):
+            one(ciphers, rng, AES128, keys[AES128][1], n, 13, iv_len)
+            one(ciphers, rng, AES256, keys[AES256][2], n, 0, iv_len)
+    # AES-192 keys through the AES-128 suite's cipher (the key length picks the rounds, gcm.rs:49)
+    k192 = bytes(rng.getrandbits(8) for _ in range(24))
+    for n in (0, 100, 1537):
+        one(ciphers, rng, AES128, k192, n, 5)
+    print("ivs and key sizes OK", flush=True)
+    for _ in range(2):  # a batch launch in between: the server stops for it, the next call starts a new one
+        batch_launch()
+        one(ciphers, rng, AES256, keys[AES256][0], 1537, 5)
+        one(ciphers, rng, CHACHA, keys[CHACHA][0], 1537, 5)
     for _ in range(3):  # the server leaves after ATLS_SINGLE_RESIDENT_IDLE_MS without a call; the next call relaunches it
         time.sleep(0.05)
-        one(c, rng, keys[0], 1537, 5)
+        one(ciphers, rng, AES128, keys[AES128][0], 1537, 5)
+        one(ciphers, rng, CHACHA, keys[CHACHA][0], 1537, 5)
+    print("relaunches OK", flush=True)
     errors = []
 
     def worker(t):
         r = random.Random(t)
         try:
-            for i in range(60):
-                one(c, r, keys[(t + i) % 3], r.choice([0, 1, 64, 700, 1537, 2048, 3000]), r.choice([0, 5, 13]))
+            for i in range(40):
+                s = (CHACHA, AES128, AES256)[(t + i) % 3]
+                one(ciphers, r, s, keys[s][(t + i) % 3], r.choice([0, 1, 64, 700, 1537, 2048, 3000]), r.choice([0, 5, 13]))
         except BaseException as ex:  # noqa: BLE001
             errors.append(ex)
 
