@@ -1155,18 +1155,37 @@ __global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
 #endif
 }
 
+#ifndef ATLS_TT_B128
+#define ATLS_TT_B128 1  // 0: the replicated T-table rows written one word per store (round 4)
+#endif
+// The replicated T-tables (row x: T0[x] x32 | T1[x] x32, T1 = rotl8 T0) at LDS address 0, by NT threads: T0
+// through the (still unused) GHASH area with one global load per thread instead of a dependent load per LDS
+// word, then each row 16 bytes per store (four copies of one entry), the loop unrolled so the row reads of
+// several stores are in flight at once. Ends with a barrier.
+template <int NT>
+__device__ __forceinline__ void build_ttables(uint32_t* smem, const uint32_t* t0, int t) {
+  for (int i = t; i < 256; i += NT) smem[kTabBytes / 4 + i] = t0[i];
+  __syncthreads();
+  if (ATLS_TT_B128) {
+#pragma unroll 8
+    for (int i = t; i < kTabBytes / 16; i += NT) {
+      const uint32_t v = smem[kTabBytes / 4 + (i >> 4)];
+      const uint32_t w = (i & 8) ? rotl32(v, 8) : v;
+      reinterpret_cast<uint4*>(smem)[i] = make_uint4(w, w, w, w);
+    }
+  } else {
+    for (int i = t; i < kTabBytes / 4; i += NT) {
+      const uint32_t v = smem[kTabBytes / 4 + (i >> 6)];
+      smem[i] = (i & 32) ? rotl32(v, 8) : v;
+    }
+  }
+  __syncthreads();
+}
+
 template <bool OPEN, int kWaves, int NR>
 __device__ __forceinline__ void gcm_kernel_body(const GcmArgs& A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  // T0 (1 KiB) through the (still unused) GHASH area: one global load per thread instead of a
-  // dependent load per LDS word of the 64 KiB replicated tables
-  if (threadIdx.x < 256) smem[kTabBytes / 4 + threadIdx.x] = A.t0[threadIdx.x];
-  __syncthreads();
-  for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
-    const uint32_t v = smem[kTabBytes / 4 + (i >> 6)];
-    smem[i] = (i & 32) ? rotl32(v, 8) : v;  // row x: T0[x] x32 | T1[x] x32
-  }
-  __syncthreads();
+  build_ttables<64 * kWaves>(smem, A.t0, (int)threadIdx.x);
   const int wave = (int)uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const uint32_t lb = 4u * (uint32_t)(lane & 31);
   const uint32_t wb = (uint32_t)kTabBytes + (ATLS_DBG_SHARED_GHASH ? 0u : (uint32_t)wave * kGhashBytes);
@@ -1255,13 +1274,7 @@ static_assert(kSingleLds <= 160u * 1024u, "the single-call kernel's LDS");
 template <bool OPEN, int NR>
 __device__ __forceinline__ void single_record(const GcmArgs& A) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  smem[kTabBytes / 4 + threadIdx.x] = A.t0[threadIdx.x];  // 256 threads: T0 through the GHASH area
-  __syncthreads();
-  for (int i = threadIdx.x; i < kTabBytes / 4; i += blockDim.x) {
-    const uint32_t v = smem[kTabBytes / 4 + (i >> 6)];
-    smem[i] = (i & 32) ? rotl32(v, 8) : v;
-  }
-  __syncthreads();
+  build_ttables<64 * kSingleWaves>(smem, A.t0, (int)threadIdx.x);
   const int t = (int)threadIdx.x;
   gcm_one<NR, OPEN, true, 64 * kSingleWaves>(A, 0u, 4u * (uint32_t)(t & 31), (uint32_t)kTabBytes, t);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -1419,12 +1432,7 @@ __global__ __launch_bounds__(64 * kSingleWaves) void single_resident(uint8_t* bl
                          (atls_open_result*)(sl + kResRes), S.q4);
     } else if constexpr (GCM) {
       if (!tables) {  // T0 through the (still unused) GHASH area, then the replicated rows (single_record)
-        smem[kTabBytes / 4 + t] = R.t0[t];
-        __syncthreads();
-        for (int i = t; i < (int)(kTabBytes / 4); i += 64 * kSingleWaves) {
-          const uint32_t x = smem[kTabBytes / 4 + (i >> 6)];
-          smem[i] = (i & 32) ? rotl32(x, 8) : x;
-        }
+        build_ttables<64 * kSingleWaves>(smem, R.t0, t);
         tables = true;
       }
       if (t == 0) {
