@@ -1361,8 +1361,9 @@ constexpr size_t kResidentLds = kSingleLds + sizeof(ResidentLds);
 static_assert(kSingleLds % 16 == 0 && kResidentLds <= 160u * 1024u, "the resident server's LDS");
 
 // GCM = false: a ChaCha20-Poly1305-only server (ATLS_SINGLE_RESIDENT=1). The server with the AES-GCM path takes
-// 217 VGPRs against 100, and its ChaCha20-Poly1305 calls measured 0.9 us slower with the keystream code
-// unchanged (profiles/r05/single/ab_resident_gcm.log), so both suites on one server is its own mode (=2).
+// 217 VGPRs against 100, and its ChaCha20-Poly1305 calls measured 0.4-0.9 us slower with the keystream code
+// unchanged (profiles/r05/single/ab_resident_gcm*.log: capping it at 128 VGPRs spills and is slower still, the
+// 10-round path alone is within noise), so both suites on one server is its own mode (=2).
 template <bool GCM>
 __global__ __launch_bounds__(64 * kSingleWaves) void single_resident(uint8_t* blk, uint32_t idle_us) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // AES-GCM: T-tables, GHASH areas (kSingleLds)
