@@ -1,8 +1,9 @@
 """Benchmark: device-resident TLS-record AEAD throughput (BASELINE.json metric) on MI355X.
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2_aes128gcm_64Ki_x_16KiB]
-(--config c1_server_https_loopback_1MiB: BASELINE config C1, the loopback through the batched socket
-path, MB/s, with the reference's per-record CPU path as cpu_baseline)
+(--config c1_server_https_loopback_1MiB: BASELINE config C1, one connection's loopback through the native
+batched socket path (atls_sb_*), MB/s, the Python mirror beside it and 64 / 256 connections under at_scale, with
+the reference's per-record CPU path as cpu_baseline)
 For N > 1 the driver launches one rank per GPU with torch.distributed.run; each rank seals
 its own pre-sharded, device-resident batch of the config (records are independent, so there
 is no data-path collective: weak scaling). One step = one atls_seal_batch over the whole
@@ -230,38 +231,58 @@ def c1_cpu_reference(body, reps):
 
 
 def run_c1(args):
-    """C1 (server_https over loopback, 1 MiB body of 64 x 16 KiB AES-128-GCM records): the batched
-    socket path on the GPU (tools/c1_loopback.py run_gpu, one WIRE batch per body) against the
-    reference's per-record CPU path over the same loop."""
+    """C1 (server_https over loopback, 1 MiB body of 64 x 16 KiB AES-128-GCM records, one connection): the
+    native batched socket path (tools/c1_loopback_native, atls_sb_*: one WIRE seal batch per body, one open batch
+    per receive round, every byte checked) is `value`; the Python mirror (tools/c1_loopback.py run_gpu,
+    anothertls_amd.stream.StreamBatch) beside it; the reference's per-record CPU path over the same loop is the
+    cpu_baseline. K steps = K bodies; the native tool warms up with K bodies first (its page-locked arenas at
+    their size). The native runs go first, before this process opens engines of its own: a second process's
+    hardware queues on the same GPU doubled the tool's flush time (1 MiB flushes are launch-latency bound)."""
+    import subprocess
+
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import c1_loopback as c1
 
+    exe = os.path.join(ROOT, "tools", "c1_loopback_native")
+
+    def native_run(reps, conns, threads):
+        out = subprocess.run([exe, str(reps), str(conns), str(threads)], capture_output=True, text=True, timeout=300)
+        if out.returncode != 0 or not out.stdout.strip():
+            return {"error": out.stderr[-300:]}
+        line = json.loads(out.stdout.strip().splitlines()[-1])
+        line.pop("config", None)
+        return line
+
+    native, scale = None, []
+    if os.path.exists(exe):
+        native = native_run(args.steps, 1, 1)
+        if not native.get("verified"):
+            raise RuntimeError(f"c1_loopback_native: {native}")
+        # C1 at scale (VERDICT r4 #5): 64 and 256 connections with worker threads; the server and client sides
+        # run in one process, so T threads per side is 2T on the host's CPU share (16 on the GPU box)
+        for conns, reps in ((64, 16), (256, 4)):
+            for threads in sorted({1, 8, args.c1_threads}):
+                scale.append(native_run(reps, conns, threads))
     body = np.random.default_rng(0xC1).integers(0, 256, c1.N_REC * c1.CONTENT, dtype=np.uint8).tobytes()
     dt, pt = c1.run_gpu(body, args.steps)
     assert pt == body
+    py = {"MBps": round(args.steps * len(body) / dt / 1e6, 1), "ms_per_step": round(dt / args.steps * 1e3, 3),
+          "warmup": 1, "path": "anothertls_amd.stream.StreamBatch (WIRE mode), Python"}
+    if native:
+        value, ms, warm = native["gpu_MBps"], native["phase_ms"]["wall"] / args.steps, args.steps
+        path = "native atls_stream_batch (include/atls.h atls_sb_*, WIRE mode), one connection, every byte checked"
+    else:  # the tool is built by __graft_entry__.build(); without it the Python mirror's rate is the value
+        value, ms, warm, path = py["MBps"], py["ms_per_step"], 1, py["path"]
     result = {"metric": "MB/s of response body through seal -> 127.0.0.1 socket -> open (server_https loopback)",
-              "value": round(args.steps * len(body) / dt / 1e6, 1), "unit": "MB/s", "n_gpus": 1,
-              "steps": args.steps, "warmup": 1, "ms_per_step": round(dt / args.steps * 1e3, 3),
+              "value": value, "unit": "MB/s", "n_gpus": 1,
+              "steps": args.steps, "warmup": warm, "ms_per_step": round(ms, 3),
               "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u8",
               "data": "synthetic 1 MiB body, RFC 8448 server traffic secret",
               "config": {"workload": C1, "records_per_body": c1.N_REC, "record_content": c1.CONTENT,
-                         "suite": "TLS_AES_128_GCM_SHA256", "path": "anothertls_amd.stream.StreamBatch (WIRE mode)"}}
-    # C1 at scale (VERDICT r4 #5): the native batched socket path (tools/c1_loopback_native, atls_sb_* with
-    # worker threads) over 64 and 256 connections, every byte checked by the tool; the server and client sides
-    # run in one process, so T threads per side is 2T on the host's CPU share (16 on the GPU box)
-    exe = os.path.join(ROOT, "tools", "c1_loopback_native")
-    if os.path.exists(exe):
-        import subprocess
-
-        scale = []
-        for conns, reps in ((64, 16), (256, 4)):
-            for threads in sorted({1, 8, args.c1_threads}):
-                out = subprocess.run([exe, str(reps), str(conns), str(threads)], capture_output=True, text=True,
-                                     timeout=300)
-                line = json.loads(out.stdout.strip().splitlines()[-1]) if out.returncode == 0 and out.stdout.strip() \
-                    else {"error": out.stderr[-300:]}
-                line.pop("config", None)
-                scale.append(line)
+                         "suite": "TLS_AES_128_GCM_SHA256", "connections": 1, "path": path},
+              "python_StreamBatch": py}
+    if native:
+        result["native_phase_ms"] = native["phase_ms"]
         result["at_scale"] = {"runs": scale, "unit": "MB/s of response body, seal -> 127.0.0.1 TCP -> open, every byte checked",
                               "path": "native atls_stream_batch: a flush seals its records in engine batches of <= 64 MiB "
                                       "while the previous batch is sent, a receive round opens in such batches; "
