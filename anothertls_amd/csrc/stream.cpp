@@ -58,10 +58,12 @@ constexpr int kBrokenPipe = 254;                  // TlsError::BrokenPipe, alert
 constexpr size_t kRecvChunk = size_t(256) << 10;  // room made in a receive buffer per recv call
 constexpr size_t kRxMax = size_t(1) << 31;        // unopened bytes per connection (record offsets are u32)
 constexpr int kMaxThreads = 64;
-// A flush or receive round goes to the engine in batches of whole connections of at most this many wire
-// bytes (one connection more than that is a batch of its own): the page-locked staging the batches use stays
-// bounded however much is queued, and a flush sends one batch while the engine seals the next.
+// A receive round goes to the engine in batches of whole connections of at most this many wire bytes (one
+// connection more than that is a batch of its own), a flush in batches of consecutive records of at most this
+// many: the page-locked staging the batches use stays bounded however much is queued, and a flush sends one
+// batch while the engine seals the next.
 constexpr size_t kBatchBytes = size_t(64) << 20;
+constexpr size_t kMinBatchBytes = size_t(8) << 20;  // a flush's smallest engine batch (if it has that much)
 
 // [c0, c1) ranges of connections whose wire bytes (prefix sums `base`) fit kBatchBytes, skipping empty ones
 std::vector<std::pair<size_t, size_t>> batch_groups(const std::vector<size_t>& base) {
@@ -500,33 +502,52 @@ long atls_sb_flush(atls_stream_batch* sb) {
     sb->in_len = 0;
     threads = sb->threads;
   }
-  // engine batches of whole connections; batch g is sealed into wire_out[g & 1] while batch g - 1 is sent
-  // from the other buffer (a connection's records are all in one batch, and batches go out in order)
-  const size_t nc = fds.size();
+  // Engine batches of consecutive records (a quarter of the flush each, 8 .. 64 MiB of wire bytes; smaller flushes
+  // are one batch: a 1 MiB flush cut into 256 KiB batches took 4x as long, each batch paying its own copies,
+  // launch and wait): batch g is sealed into wire_out[g & 1] while batch g - 1 is sent from the other buffer. A connection's bytes go out in order: its parts in batch g - 1 are
+  // sent before batch g's, and a connection whose send failed sends nothing more.
+  const size_t nc = fds.size(), total = wbase[nc];
+  const size_t target = std::min(kBatchBytes, std::max(kMinBatchBytes, total / 4));
+  std::vector<size_t> gs{0};  // first record of each batch, then n
+  for (size_t r = 0, acc = 0; r < n; r++) {
+    const size_t w = (size_t)sb->frecs[r].len + 22u;
+    if (acc && acc + w > target) {
+      gs.push_back(r);
+      acc = 0;
+    }
+    acc += w;
+  }
+  gs.push_back(n);
+  std::vector<size_t> gw(gs.size());  // the batches' first wire bytes, then total
+  for (size_t g = 0; g + 1 < gs.size(); g++) gw[g] = sb->frecs[gs[g]].out_off;
+  gw.back() = total;
   std::vector<char> failed(nc, 0);
-  const auto groups = batch_groups(wbase);
   std::thread sender;
   int rc = ATLS_OK;
   size_t g = 0;
   Stopwatch sw;
-  for (; g < groups.size(); g++) {
-    const size_t c0 = groups[g].first, c1 = groups[g].second;
+  for (; g + 1 < gs.size(); g++) {
+    const size_t r0 = gs[g], r1 = gs[g + 1], w0 = gw[g], w1 = gw[g + 1];
     Pinned& out = sb->wire_out[g & 1];
-    if (!out.reserve(wbase[c1] - wbase[c0] + 16)) {
+    if (!out.reserve(w1 - w0 + 16)) {
       rc = ATLS_INTERNAL_ERROR;
       break;
     }
-    for (size_t r = rbase[c0]; r < rbase[c1]; r++) sb->frecs[r].out_off -= wbase[c0];
-    rc = atls_seal_batch(sb->e, sb->frecs.data() + rbase[c0], (uint32_t)(rbase[c1] - rbase[c0]), arena->p, nullptr,
-                         out.p, nullptr, 0);
+    for (size_t r = r0; r < r1; r++) sb->frecs[r].out_off -= w0;
+    rc = atls_seal_batch(sb->e, sb->frecs.data() + r0, (uint32_t)(r1 - r0), arena->p, nullptr, out.p, nullptr, 0);
     if (rc) break;
     sb->t_seal += sw.lap();
     if (sender.joinable()) sender.join();
-    sender = std::thread([&, c0, c1, wire = out.p] {
-      parallel(threads, c1 - c0, [&](size_t k) {
-        const size_t ci = c0 + k;
-        if (dead[ci] || wbase[ci + 1] == wbase[ci]) return;
-        if (!send_all(fds[ci], wire + wbase[ci] - wbase[c0], wbase[ci + 1] - wbase[ci])) failed[ci] = 1;
+    // the connections with bytes in [w0, w1): c_lo .. c_hi - 1
+    const size_t c_lo = (size_t)(std::upper_bound(wbase.begin(), wbase.end(), w0) - wbase.begin()) - 1;
+    size_t c_hi = c_lo;
+    while (c_hi < nc && wbase[c_hi] < w1) c_hi++;
+    sender = std::thread([&, c_lo, c_hi, w0, w1, wire = out.p] {
+      parallel(threads, c_hi - c_lo, [&](size_t k) {
+        const size_t ci = c_lo + k;
+        const size_t lo = std::max(wbase[ci], w0), hi = std::min(wbase[ci + 1], w1);
+        if (dead[ci] || failed[ci] || hi <= lo) return;
+        if (!send_all(fds[ci], wire + (lo - w0), hi - lo)) failed[ci] = 1;
       });
     });
   }
@@ -538,7 +559,7 @@ long atls_sb_flush(atls_stream_batch* sb) {
       Conn& c = sb->conns[ci];
       if (failed[ci] && !c.err) c.err = kBrokenPipe;
       // records of batches the engine did not seal are lost: their connections end with the engine's error
-      if (rc && g < groups.size() && ci >= groups[g].first && wbase[ci + 1] != wbase[ci] && !c.err) c.err = rc;
+      if (rc && g + 1 < gs.size() && wbase[ci + 1] > gw[g] && wbase[ci + 1] != wbase[ci] && !c.err) c.err = rc;
       publish_err(c);
     }
   }

@@ -261,9 +261,9 @@ void atls_partition(const atls_rec* recs, uint32_t n, int open, uint32_t parts, 
 /* ---- Batched record streams (TlsStream::tls_write / tls_read, net/stream.rs:32-150) -------
  * Many connections over one engine: atls_sb_write queues a connection's records (fragmented at
  * 2^14 bytes, RFC 8446 §5.1; the data is copied once, into the batch's page-locked input), atls_sb_flush
- * seals the queued records of every connection in ATLS_MODE_WIRE batches of whole connections (<= 64 MiB of
- * wire bytes each, one sealed while the previous one is sent) and send()s each connection's wire bytes in
- * order; received bytes (atls_sb_recv / atls_sb_recv_all from the sockets, or atls_sb_feed) are
+ * seals the queued records of every connection in ATLS_MODE_WIRE batches of consecutive records (a quarter of
+ * the flush each, 8 .. 64 MiB of wire bytes, one sealed while the previous one is sent) and send()s each
+ * connection's wire bytes in order; received bytes (atls_sb_recv / atls_sb_recv_all from the sockets, or atls_sb_feed) are
  * split into whole records (Record::from_raw, record.rs:81-102), atls_sb_open_pending opens every
  * connection's complete records in one batch, atls_sb_read returns the next application-data record of a
  * connection (blocking: receives and opens as needed; UnexpectedMessage (10) for other content types,
