@@ -504,8 +504,9 @@ long atls_sb_flush(atls_stream_batch* sb) {
   }
   // Engine batches of consecutive records (a quarter of the flush each, 8 .. 64 MiB of wire bytes; smaller flushes
   // are one batch: a 1 MiB flush cut into 256 KiB batches took 4x as long, each batch paying its own copies,
-  // launch and wait): batch g is sealed into wire_out[g & 1] while batch g - 1 is sent from the other buffer. A connection's bytes go out in order: its parts in batch g - 1 are
-  // sent before batch g's, and a connection whose send failed sends nothing more.
+  // launch and wait): batch g is sealed into wire_out[g & 1] while batch g - 1 is sent from the other buffer. A
+  // connection's bytes go out in order: its part of batch g - 1 is sent before its part of batch g, and a
+  // connection whose send failed sends nothing more.
   const size_t nc = fds.size(), total = wbase[nc];
   const size_t target = std::min(kBatchBytes, std::max(kMinBatchBytes, total / 4));
   std::vector<size_t> gs{0};  // first record of each batch, then n
