@@ -563,6 +563,14 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
                  "plaintext_and_status_ok": ok,
                  "what": "open_batch over the sealed records (device-resident, same batch), HIP events on the "
                          "engine stream over the timed steps"}
+    if m.get("lds"):
+        # the open kernels' own clock: in cycles they are within ~2 % of the seal's, and the PMC put their clock
+        # 8-13 % lower (profiles/r05/pmc_open/), so the open's LDS-array fraction is stated at its own clock
+        osclk = clock_pass(eng, dev, lambda: eng.open_batch(q_recs, p_out, p_aux, p_tags, q_pt, q_res, flags=flags, n=n),
+                           steps, open_ms)
+        ol = lds_roofline(batch, open_ms, osclk, torch.cuda.get_device_properties(dev).multi_processor_count)
+        if ol:
+            m["open"]["lds"] = {"sclk_MHz": ol["sclk_MHz"], "t_min_ms": ol["t_min_ms"], "frac": ol["frac"]}
     del d_orecs, d_pt, d_res
     if keep:
         m.update(d_in=d_in, d_out=d_out, d_tags=d_tags, d_aux=d_aux, d_recs=d_recs)
