@@ -24,7 +24,8 @@ Fields beyond the driver contract:
                  tag per record (ATLS_MODE_WIRE), payload GiB/s from HIP events.
   open         — the decrypt half: open_batch over the sealed records of the same batch (GiB/s,
                  kernel_ms from HIP events, roofline frac with the same 2L+16 bytes per record),
-                 statuses, lengths and (uniform configs) every plaintext byte checked.
+                 statuses, lengths and (uniform configs) every plaintext byte checked; AES-GCM configs
+                 add open.lds, the open kernels' LDS-array fraction at their own measured clock.
   cpu_baseline — the oracle (literal C restatement of the reference's algorithm: byte S-box
                  AES with bit-serial MixColumns, bit-serial GHASH) on a bounded sample of the
                  same records, on this host: --cpu-threads threads (value) and 1 thread
