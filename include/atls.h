@@ -139,7 +139,11 @@ typedef struct atls_engine atls_engine;
  * Host pointers; device 0 or $ATLS_DEVICE. Reentrant and concurrent (Cipher is Send + Sync): a call
  * leases one of at most $ATLS_SINGLE_CONTEXTS (8) call contexts -- engines, streams, a mapped pinned
  * block the kernel reads and writes in place -- and callers beyond that wait for one; a context keeps
- * the device key schedules of its last 16 keys per key size, so repeated keys cost no key setup. */
+ * the device key schedules of its last 16 keys per key size, so repeated keys cost no key setup.
+ * $ATLS_SINGLE_RESIDENT=1 (opt-in): ChaCha20-Poly1305 calls whose IV || AAD || input fit 3,584 B go to one
+ * workgroup that stays on the GPU and answers through a doorbell in mapped memory (no launch per call); =2:
+ * AES-GCM calls too. The server leaves after $ATLS_SINGLE_RESIDENT_IDLE_MS (20) without a call, and the
+ * process stops it before each launch of its own (a running kernel holds a hardware queue). */
 int atls_seal(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t* iv, size_t iv_len,
               const uint8_t* aad, size_t aad_len, const uint8_t* in, size_t len, uint8_t* out,
               uint8_t tag[16]);
