@@ -834,7 +834,7 @@ int cached_slot(SingleCtx* c, uint16_t suite, const uint8_t* key, size_t key_len
 
 // ---- the resident single-call server (opt-in) ----
 // ATLS_SINGLE_RESIDENT: 1 = ChaCha20-Poly1305 calls through the server, 2 = AES-GCM calls too (the server with
-// the AES-GCM path serves ChaCha20-Poly1305 0.9 us slower: profiles/r05/single/ab_resident_gcm.log)
+// the AES-GCM path serves ChaCha20-Poly1305 0-0.3 us slower: profiles/r05/single/resident_modes_noscratch.log)
 int resident_mode() {
   static const int v = [] {
     const char* e = std::getenv("ATLS_SINGLE_RESIDENT");

@@ -1360,10 +1360,11 @@ struct ResidentLds {
 constexpr size_t kResidentLds = kSingleLds + sizeof(ResidentLds);
 static_assert(kSingleLds % 16 == 0 && kResidentLds <= 160u * 1024u, "the resident server's LDS");
 
-// GCM = false: a ChaCha20-Poly1305-only server (ATLS_SINGLE_RESIDENT=1). The server with the AES-GCM path takes
-// 217 VGPRs against 100, and its ChaCha20-Poly1305 calls measured 0.4-0.9 us slower with the keystream code
-// unchanged (profiles/r05/single/ab_resident_gcm*.log: capping it at 128 VGPRs spills and is slower still, the
-// 10-round path alone is within noise), so both suites on one server is its own mode (=2).
+// GCM = false: a ChaCha20-Poly1305-only server (ATLS_SINGLE_RESIDENT=1); GCM = true serves both suites (=2). The
+// server with the AES-GCM path (217 VGPRs against 100) first kept the request header in registers and spilled two
+// of its fields to scratch on every request: its ChaCha20-Poly1305 calls were 0.9 us slower
+// (profiles/r05/single/ab_resident_gcm*.log). With the header read from LDS where it is used the difference is
+// 0-0.3 us (resident_modes_noscratch.log).
 template <bool GCM>
 __global__ __launch_bounds__(64 * kSingleWaves) void single_resident(uint8_t* blk, uint32_t idle_us) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];  // AES-GCM: T-tables, GHASH areas (kSingleLds)
@@ -1419,12 +1420,16 @@ __global__ __launch_bounds__(64 * kSingleWaves) void single_resident(uint8_t* bl
     if (t < kIn) stage_in[t] = ((const uint4*)(sl + kResBytes))[t];
     else if (t < kIn + kHdr) hdr[t - kIn] = ((const uint4*)(sl + kResReq))[t - kIn];
     __syncthreads();  // (also: every wave has read the command before wave 0 may overwrite it)
-    ResidentReq R;
-    __builtin_memcpy(&R, hdr, sizeof R);
-    const uint32_t nr = __builtin_amdgcn_readfirstlane(R.nr), open = __builtin_amdgcn_readfirstlane(R.open);
-    atls_rec dl = R.d;
-    dl.out_off = 0;
+    // the request header stays in LDS: each path reads its fields where it uses them (copied into registers up
+    // front, the AES-GCM path's fields were spilled to scratch on every request)
+    const ResidentReq& RL = *reinterpret_cast<const ResidentReq*>(hdr);
+    const uint32_t nr = __builtin_amdgcn_readfirstlane(RL.nr), open = __builtin_amdgcn_readfirstlane(RL.open);
+    const uint32_t rlen = __builtin_amdgcn_readfirstlane(RL.d.len);
     if (nr == 0) {
+      ResidentReq R;
+      __builtin_memcpy(&R, hdr, sizeof R);
+      atls_rec dl = R.d;
+      dl.out_off = 0;
       if (open)
         q4_record<true>(R.ks, dl, (const uint8_t*)stage_in, R.tag_off, (uint8_t*)stage_out, sl + kResTag,
                         (atls_open_result*)(sl + kResRes), S.q4);
@@ -1433,29 +1438,30 @@ __global__ __launch_bounds__(64 * kSingleWaves) void single_resident(uint8_t* bl
                          (atls_open_result*)(sl + kResRes), S.q4);
     } else if constexpr (GCM) {
       if (!tables) {  // T0 through the (still unused) GHASH area, then the replicated rows (single_record)
-        build_ttables<64 * kSingleWaves>(smem, R.t0, t);
+        build_ttables<64 * kSingleWaves>(smem, RL.t0, t);
         tables = true;
       }
-      if (t == 0) {
-        dl.key_slot = 0;
-        rec = dl;
+      if (t == 0) {  // the descriptor gcm_one reads: out_off indexes the reply, the slot's schedule is ks
+        rec = RL.d;
+        rec.out_off = 0;
+        rec.key_slot = 0;
       }
       __syncthreads();
       const uint8_t* in = (const uint8_t*)stage_in;
       uint8_t* out = (uint8_t*)stage_out;
       if (nr == 10) {
-        if (open) resident_gcm<10, true>(R, &rec, in, out, sl);
-        else resident_gcm<10, false>(R, &rec, in, out, sl);
+        if (open) resident_gcm<10, true>(RL, &rec, in, out, sl);
+        else resident_gcm<10, false>(RL, &rec, in, out, sl);
       } else if (nr == 12) {
-        if (open) resident_gcm<12, true>(R, &rec, in, out, sl);
-        else resident_gcm<12, false>(R, &rec, in, out, sl);
+        if (open) resident_gcm<12, true>(RL, &rec, in, out, sl);
+        else resident_gcm<12, false>(RL, &rec, in, out, sl);
       } else {
-        if (open) resident_gcm<14, true>(R, &rec, in, out, sl);
-        else resident_gcm<14, false>(R, &rec, in, out, sl);
+        if (open) resident_gcm<14, true>(RL, &rec, in, out, sl);
+        else resident_gcm<14, false>(RL, &rec, in, out, sl);
       }
     }
     __syncthreads();  // the reply is whole in LDS
-    const uint32_t nout = (R.d.len + 15u) / 16u;
+    const uint32_t nout = (rlen + 15u) / 16u;
     for (uint32_t i = (uint32_t)t; i < nout; i += 64u * kSingleWaves) ((uint4*)(sl + kResOut))[i] = stage_out[i];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
