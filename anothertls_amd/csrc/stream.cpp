@@ -49,6 +49,7 @@
 
 #include "../../include/atls.h"
 #include "record_split.h"
+#include "stream_batches.h"
 
 namespace {
 
@@ -58,27 +59,6 @@ constexpr int kBrokenPipe = 254;                  // TlsError::BrokenPipe, alert
 constexpr size_t kRecvChunk = size_t(256) << 10;  // room made in a receive buffer per recv call
 constexpr size_t kRxMax = size_t(1) << 31;        // unopened bytes per connection (record offsets are u32)
 constexpr int kMaxThreads = 64;
-// A receive round goes to the engine in batches of whole connections of at most this many wire bytes (one
-// connection more than that is a batch of its own), a flush in batches of consecutive records of at most this
-// many: the page-locked staging the batches use stays bounded however much is queued, and a flush sends one
-// batch while the engine seals the next.
-constexpr size_t kBatchBytes = size_t(64) << 20;
-constexpr size_t kMinBatchBytes = size_t(8) << 20;  // a flush's smallest engine batch (if it has that much)
-
-// [c0, c1) ranges of connections whose wire bytes (prefix sums `base`) fit kBatchBytes, skipping empty ones
-std::vector<std::pair<size_t, size_t>> batch_groups(const std::vector<size_t>& base) {
-  std::vector<std::pair<size_t, size_t>> g;
-  const size_t nc = base.size() - 1;
-  for (size_t c0 = 0; c0 < nc;) {
-    while (c0 < nc && base[c0 + 1] == base[c0]) c0++;
-    if (c0 == nc) break;
-    size_t c1 = c0 + 1;
-    while (c1 < nc && base[c1 + 1] - base[c0] <= kBatchBytes) c1++;
-    g.emplace_back(c0, c1);
-    c0 = c1;
-  }
-  return g;
-}
 
 // Grow-only page-locked host buffer: the engine's copies from it run at full PCIe speed. keep: bytes
 // [0, keep) survive a growth (the write arena fills across several writes).
@@ -350,7 +330,7 @@ long open_pending_locked(atls_stream_batch* sb) {
   if (n > 0xffffffffu) return -ATLS_ILLEGAL_PARAMETER;
   const int rc = install_keys(sb);
   if (rc) return -rc;
-  for (const auto& g : batch_groups(wbase)) {  // a connection that has records pending has wire bytes
+  for (const auto& g : atls_stream::connection_batches(wbase)) {  // a connection that has records pending has wire bytes
     const long got = open_group(sb, g.first, g.second, wbase, rbase);
     if (got < 0) return got;
   }
@@ -508,17 +488,8 @@ long atls_sb_flush(atls_stream_batch* sb) {
   // connection's bytes go out in order: its part of batch g - 1 is sent before its part of batch g, and a
   // connection whose send failed sends nothing more.
   const size_t nc = fds.size(), total = wbase[nc];
-  const size_t target = std::min(kBatchBytes, std::max(kMinBatchBytes, total / 4));
-  std::vector<size_t> gs{0};  // first record of each batch, then n
-  for (size_t r = 0, acc = 0; r < n; r++) {
-    const size_t w = (size_t)sb->frecs[r].len + 22u;
-    if (acc && acc + w > target) {
-      gs.push_back(r);
-      acc = 0;
-    }
-    acc += w;
-  }
-  gs.push_back(n);
+  const std::vector<size_t> gs = atls_stream::record_batches(  // first record of each batch, then n
+      n, atls_stream::flush_target(total), [&](size_t r) { return (size_t)sb->frecs[r].len + 22u; });
   std::vector<size_t> gw(gs.size());  // the batches' first wire bytes, then total
   for (size_t g = 0; g + 1 < gs.size(); g++) gw[g] = sb->frecs[gs[g]].out_off;
   gw.back() = total;
@@ -539,10 +510,8 @@ long atls_sb_flush(atls_stream_batch* sb) {
     if (rc) break;
     sb->t_seal += sw.lap();
     if (sender.joinable()) sender.join();
-    // the connections with bytes in [w0, w1): c_lo .. c_hi - 1
-    const size_t c_lo = (size_t)(std::upper_bound(wbase.begin(), wbase.end(), w0) - wbase.begin()) - 1;
-    size_t c_hi = c_lo;
-    while (c_hi < nc && wbase[c_hi] < w1) c_hi++;
+    const auto cr = atls_stream::connections_in(wbase, w0, w1);  // the connections with bytes in [w0, w1)
+    const size_t c_lo = cr.first, c_hi = cr.second;
     sender = std::thread([&, c_lo, c_hi, w0, w1, wire = out.p] {
       parallel(threads, c_hi - c_lo, [&](size_t k) {
         const size_t ci = c_lo + k;

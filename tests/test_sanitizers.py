@@ -4,7 +4,9 @@ sanitizers"; GPU sanitizers are not available on this pool):
 * the socket path's record splitter (anothertls_amd/csrc/record_split.h, which stream.cpp uses to
   split untrusted received bytes) fed randomized record streams in random chunks, against the
   mirror of the reference's Record::from_raw (anothertls_amd/record.py, net/record.rs:81-102);
-* the oracle (oracle/ref_restatement.c) over every entry point (tests/native/oracle_asan.c).
+* the oracle (oracle/ref_restatement.c) over every entry point (tests/native/oracle_asan.c);
+* how the socket path cuts flushes and receive rounds into engine batches (anothertls_amd/csrc/stream_batches.h)
+  on random connection / record layouts (tests/native/batches_fuzz.cpp).
 """
 import fcntl
 import os
@@ -91,3 +93,9 @@ def test_split_fuzz_matches_from_raw(san_build):
         assert got == want, (it, got, want)
         assert (err[0] if err else None) == werr, (it, err, werr)
         assert left == wleft, (it, left, wleft)
+
+
+def test_stream_batches_fuzz(san_build):
+    r = subprocess.run([os.path.join(san_build, "batches_fuzz_san")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "OK" in r.stdout
