@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -436,13 +437,15 @@ int run_host_pipelined(atls_engine* e, bool open, const atls_rec* recs, uint32_t
   return finish(e, 0, true);
 }
 
-void resident_yield();  // below, with the resident single-call server
+using atls::ResidentHold;  // engine_internal.h; defined below, with the resident single-call server
+
+unsigned long long g_host_unpipelined = 0;  // host batches staged in one piece: records out of order (diagnostic)
 
 int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
               void* out, uint8_t* tags_out, const uint8_t* tags_in, atls_open_result* res, uint32_t flags) {
   if (!e) return ATLS_INTERNAL_ERROR;
   if (n == 0) return ATLS_OK;
-  resident_yield();
+  ResidentHold hold;
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
   if (e->n_slots == 0) return ATLS_ILLEGAL_PARAMETER;
@@ -521,6 +524,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     if (!planned && n > 1 && !e->no_pipeline) {
       const int rc = run_host_pipelined(e, open, recs, n, in, aux, out, tags_out, tags_in, res, in_end, out_end, aux_end);
       if (rc != -1) return rc;
+      __atomic_fetch_add(&g_host_unpipelined, 1ull, __ATOMIC_RELAXED);
     }
     if (in_end && hipMemcpyAsync(e->in.p, in, in_end, hipMemcpyHostToDevice, s) != hipSuccess) return ATLS_INTERNAL_ERROR;
     if (aux_end && hipMemcpyAsync(e->aux.p, aux, aux_end, hipMemcpyHostToDevice, s) != hipSuccess)
@@ -635,7 +639,7 @@ int key_status(const atls_key& k) {
 // (the table grows, keeping the other slots); replace = the table becomes exactly these n slots.
 // Caller holds e->mu.
 int install_keys(atls_engine* e, uint32_t first, const atls_key* keys, uint32_t n, bool replace) {
-  resident_yield();
+  ResidentHold hold;
   int status = ATLS_OK;
   for (uint32_t i = 0; i < n && status == ATLS_OK; i++) status = key_status(keys[i]);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
@@ -915,8 +919,8 @@ int resident_slot(SingleCtx* c, atls_engine* e) {
       return -1;
     }
     std::memset(p, 0, kResBlock);
-    S.h = (uint8_t*)p;
     S.d = (uint8_t*)pd;
+    __atomic_store_n(&S.h, (uint8_t*)p, __ATOMIC_RELEASE);  // ResidentHold reads it without S.mu
     S.dev = e->device;
     std::atexit(stop_resident);
   }
@@ -926,13 +930,19 @@ int resident_slot(SingleCtx* c, atls_engine* e) {
 }
 
 // A running server holds its hardware queue (GPU_MAX_HW_QUEUES is 4 per process), so any other kernel of the
-// process whose stream maps to that queue would wait for the server's idle timeout: before a launch of its
-// own, the process stops the server (stop word, wait for alive == 0, clear the word); the next resident call
-// starts it again.
-void resident_yield() {
-  if (!resident_enabled()) return;
-  ResidentServer& S = resident_server();
-  if (!S.h || __atomic_load_n((const uint32_t*)(S.h + kResAlive), __ATOMIC_SEQ_CST) == 0) return;
+// process whose stream maps to that queue would wait for the server's idle timeout. Every entry point that
+// launches work of its own therefore holds a ResidentHold from before its first launch until it returns: the
+// hold counts itself in g_res_holds and stops a running server (stop word, wait for alive == 0, clear the word);
+// while any hold is live no call relaunches the server (resident_launch_locked refuses, and the call takes the
+// launch path instead), so a batch can neither be overtaken by a relaunch between its yield and its own
+// launches nor wait behind a server kept alive by other threads' calls. The
+// count is raised before S.mu is taken and a relaunch reads it under S.mu, so either the relaunch sees the hold
+// or the hold's stop sees the relaunched server.
+std::atomic<int> g_res_holds{0};
+unsigned long long g_res_fallbacks = 0;  // calls that found the server busy and took the launch path
+constexpr int kResidentBusy = -1;  // resident_call: a launch of the process is in flight, use the launch path
+
+void resident_stop(ResidentServer& S) {
   std::lock_guard<std::mutex> lk(S.mu);
   uint32_t* alive = (uint32_t*)(S.h + kResAlive);
   uint32_t* stop = (uint32_t*)(S.h + kResStopAt);
@@ -946,16 +956,26 @@ void resident_yield() {
   __atomic_store_n(stop, 0u, __ATOMIC_SEQ_CST);
 }
 
-// Launches the server unless it runs (caller holds S.mu). The kernel's last store is alive := 0, so a
-// server seen alive == 0 is gone or about to be; a new one on the same stream starts after it.
+// ResidentHold's constructor and destructor (engine_internal.h) use these; they follow the anonymous namespace.
+void resident_hold_begin() {
+  if (!resident_enabled()) return;
+  g_res_holds.fetch_add(1, std::memory_order_seq_cst);
+  ResidentServer& S = resident_server();
+  if (__atomic_load_n(&S.h, __ATOMIC_ACQUIRE)) resident_stop(S);
+}
+
+// Launches the server unless it runs (caller holds S.mu); kResidentBusy while a hold is live. The kernel's last
+// store is alive := 0, so a server seen alive == 0 is gone or about to be; a new one on the same stream starts
+// after it.
 int resident_launch_locked(ResidentServer& S) {
   if (__atomic_load_n((uint32_t*)(S.h + kResAlive), __ATOMIC_SEQ_CST) != 0) return ATLS_OK;
+  if (g_res_holds.load(std::memory_order_seq_cst) > 0) return kResidentBusy;
   __atomic_store_n((uint32_t*)(S.h + kResAlive), 1u, __ATOMIC_SEQ_CST);
   return atls_launch_single_resident(S.d, resident_idle_us(), resident_mode() == 2 ? 1 : 0, S.s);
 }
 
 // One call through the server: request into the context's slot, doorbell, then the slot's flag. Returns
-// ATLS_OK (outputs in the slot) or ATLS_INTERNAL_ERROR.
+// ATLS_OK (outputs in the slot), kResidentBusy (not served: take the launch path) or ATLS_INTERNAL_ERROR.
 int resident_call(SingleCtx* c, const void* ks, const atls_rec& d, const uint8_t* bytes, uint32_t nbytes, uint32_t tag_off,
                   bool open, uint32_t nr, const void* t0tab, void* err) {
   ResidentServer& S = resident_server();
@@ -969,9 +989,17 @@ int resident_call(SingleCtx* c, const void* ks, const atls_rec& d, const uint8_t
   const uint32_t* alive = (const uint32_t*)(S.h + kResAlive);
   __atomic_store_n(flag, v - 1u, __ATOMIC_RELEASE);  // pending: doorbell != flag
   __atomic_store_n((uint32_t*)(h + kResBell), v, __ATOMIC_SEQ_CST);
+  // A relaunch refused because a launch of the process is in flight: no server runs (alive == 0 and the hold's
+  // stop waited for the kernel to end), so the request is withdrawn (flag := doorbell, nothing pending for a
+  // later server) and the call goes down the launch path.
+  auto relaunch = [&]() -> int {
+    const int rc = resident_launch_locked(S);
+    if (rc == kResidentBusy) __atomic_store_n(flag, v, __ATOMIC_RELEASE);
+    return rc == kResidentBusy ? kResidentBusy : rc ? ATLS_INTERNAL_ERROR : ATLS_OK;
+  };
   if (__atomic_load_n(alive, __ATOMIC_SEQ_CST) == 0) {
     std::lock_guard<std::mutex> lk(S.mu);
-    if (resident_launch_locked(S)) return ATLS_INTERNAL_ERROR;
+    if (const int rc = relaunch()) return rc;
   }
   const auto t0 = std::chrono::steady_clock::now();
   for (uint64_t i = 1;; i++) {
@@ -980,7 +1008,8 @@ int resident_call(SingleCtx* c, const void* ks, const atls_rec& d, const uint8_t
       // the server left (idle) before it saw this call: its flag stores precede alive := 0, so look once more
       if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return ATLS_OK;
       std::lock_guard<std::mutex> lk(S.mu);
-      if (resident_launch_locked(S)) return ATLS_INTERNAL_ERROR;
+      if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return ATLS_OK;
+      if (const int rc = relaunch()) return rc;
     }
     if ((i & 4095) == 0) {
       const hipError_t qs = hipStreamQuery(S.s);
@@ -1108,23 +1137,27 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
     const bool chacha = suite == ATLS_TLS_CHACHA20_POLY1305_SHA256;
     rc = resident_call(c, (const atls::KeySched*)e->ks.p + slot, d, bytes, (uint32_t)(inl_tag + (open ? 16 : 0)),
                        (uint32_t)inl_tag, open, chacha ? 0u : (uint32_t)key_len / 4u + 6u, e->t0.p, e->err.p);
-    if (rc) return rc;
-    if (!open) {
-      if (std::memcmp(rh + kResTag, kTagCanary, 16) == 0) return ATLS_ILLEGAL_PARAMETER;
+    if (rc != kResidentBusy) {
+      if (rc) return rc;
+      if (!open) {
+        if (std::memcmp(rh + kResTag, kTagCanary, 16) == 0) return ATLS_ILLEGAL_PARAMETER;
+        if (len) std::memcpy(out, rh + kResOut, len);
+        std::memcpy(tag_out, rh + kResTag, 16);
+        return ATLS_OK;
+      }
+      atls_open_result res;
+      std::memcpy(&res, rh + kResRes, sizeof res);
+      if (res.status != ATLS_OK) {
+        if (len) std::memset(out, 0, len);
+        return res.status;
+      }
       if (len) std::memcpy(out, rh + kResOut, len);
-      std::memcpy(tag_out, rh + kResTag, 16);
       return ATLS_OK;
     }
-    atls_open_result res;
-    std::memcpy(&res, rh + kResRes, sizeof res);
-    if (res.status != ATLS_OK) {
-      if (len) std::memset(out, 0, len);
-      return res.status;
-    }
-    if (len) std::memcpy(out, rh + kResOut, len);
-    return ATLS_OK;
+    // busy: another thread's launch is in flight (a batch, a key install); this call is launched like it
+    __atomic_fetch_add(&g_res_fallbacks, 1ull, __ATOMIC_RELAXED);
   }
-  resident_yield();
+  ResidentHold hold;
   uint8_t* hd = c->pin_dev;
   const uint32_t done_val = ++c->calls;
   // the flag word holds anything after a (re)allocation of the block: set it to a value other than
@@ -1192,6 +1225,13 @@ int single(bool open, uint16_t suite, const uint8_t* key, size_t key_len, const 
 
 }  // namespace
 
+atls::ResidentHold::ResidentHold() : active(resident_enabled()) {
+  if (active) resident_hold_begin();
+}
+atls::ResidentHold::~ResidentHold() {
+  if (active) g_res_holds.fetch_sub(1, std::memory_order_seq_cst);
+}
+
 uint32_t atls::engine_slots(atls_engine* e) {
   if (!e) return 0;
   std::lock_guard<std::mutex> lk(e->mu);
@@ -1206,6 +1246,7 @@ const char* atls_device_arch(void) { return "gfx950"; }
 atls_engine* atls_engine_create(int device) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return nullptr;
+  ResidentHold hold;  // the T-table build below is a launch
   atls_engine* e = new (std::nothrow) atls_engine();
   if (!e) return nullptr;
   e->device = device;
@@ -1245,6 +1286,7 @@ atls_engine* atls_engine_create(int device) {
 
 void atls_engine_destroy(atls_engine* e) {
   if (!e) return;
+  ResidentHold hold;  // its streams' last kernels must not sit behind a running server
   (void)hipSetDevice(e->device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
@@ -1268,6 +1310,7 @@ void atls_engine_destroy(atls_engine* e) {
 
 int atls_engine_sync(atls_engine* e) {
   if (!e) return ATLS_INTERNAL_ERROR;
+  ResidentHold hold;  // finish may launch the completion-flag kernel
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
   return finish(e, 0);
@@ -1319,7 +1362,7 @@ int atls_open(uint16_t suite, const uint8_t* key, size_t key_len, const uint8_t*
 int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, size_t secret_len, uint32_t n,
                      atls_key* out_keys) {
   if (!e) return ATLS_INTERNAL_ERROR;
-  resident_yield();
+  ResidentHold hold;
   if (suite != ATLS_TLS_AES_128_GCM_SHA256 && suite != ATLS_TLS_AES_256_GCM_SHA384 &&
       suite != ATLS_TLS_CHACHA20_POLY1305_SHA256)
     return ATLS_INSUFFICIENT_SECURITY;
@@ -1341,7 +1384,7 @@ int atls_derive_keys(atls_engine* e, uint16_t suite, const uint8_t* secrets, siz
 int atls_hash_batch(atls_engine* e, int op, uint32_t hash_len, const uint8_t* data, size_t data_len,
                     const atls_span* keys, const atls_span* msgs, uint32_t n, uint32_t out_len, uint8_t* out) {
   if (!e) return ATLS_INTERNAL_ERROR;
-  resident_yield();
+  ResidentHold hold;
   if ((hash_len != 32 && hash_len != 48) || op < ATLS_HASH_SHA || op > ATLS_HASH_HKDF_EXPAND || !msgs ||
       (op != ATLS_HASH_SHA && !keys))
     return ATLS_ILLEGAL_PARAMETER;
@@ -1373,7 +1416,7 @@ int atls_hash_batch(atls_engine* e, int op, uint32_t hash_len, const uint8_t* da
 int atls_key_schedule(atls_engine* e, uint32_t hash_len, const uint8_t* shared, size_t shared_len,
                       const uint8_t* hello_hashes, const uint8_t* handshake_hashes, uint32_t n, uint8_t* out) {
   if (!e) return ATLS_INTERNAL_ERROR;
-  resident_yield();
+  ResidentHold hold;
   if ((hash_len != 32 && hash_len != 48) || !shared || !hello_hashes || shared_len > 1024) return ATLS_ILLEGAL_PARAMETER;
   if (n == 0) return ATLS_OK;
   std::lock_guard<std::mutex> lk(e->mu);
@@ -1398,7 +1441,7 @@ int atls_key_schedule(atls_engine* e, uint32_t hash_len, const uint8_t* shared, 
 int atls_aes_blocks(atls_engine* e, int decrypt, uint32_t key_slot, const void* in, void* out, size_t nblocks,
                     uint32_t flags) {
   if (!e) return ATLS_INTERNAL_ERROR;
-  resident_yield();
+  ResidentHold hold;
   if (nblocks == 0) return ATLS_OK;
   std::lock_guard<std::mutex> lk(e->mu);
   if (!set_dev(e)) return ATLS_INTERNAL_ERROR;
@@ -1448,6 +1491,17 @@ int atls_aes_block(int decrypt, const uint8_t* key, size_t key_len, const uint8_
 
 // Debug: copy key slot `slot`'s device key schedule (atls_dev.h KeySched, 3,648 B) to host, for the tests
 // of the key-setup kernel against a host model (tests/test_gpu_keysetup.py). Returns its size or -1.
+// Host-memory batches that could not be pipelined because their records were out of order (staged in one piece).
+extern "C" unsigned long long atls_debug_host_unpipelined(void) {
+  return __atomic_load_n(&g_host_unpipelined, __ATOMIC_RELAXED);
+}
+
+// Single calls that found the resident server held by another thread's launch and took the launch path instead
+// (tests/helpers/resident_check.py).
+extern "C" unsigned long long atls_debug_resident_fallbacks(void) {
+  return __atomic_load_n(&g_res_fallbacks, __ATOMIC_RELAXED);
+}
+
 extern "C" int atls_debug_key_sched(atls_engine* e, uint32_t slot, void* out, size_t cap) {
   if (!e || !out || cap < sizeof(atls::KeySched)) return -1;
   std::lock_guard<std::mutex> lk(e->mu);

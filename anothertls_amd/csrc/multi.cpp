@@ -536,11 +536,13 @@ int atls_multi_set_keys(atls_multi* m, const atls_key* keys, uint32_t n) {
 
 int atls_multi_seal_batch(atls_multi* m, const atls_rec* recs, uint32_t n, const void* in, const void* aux, void* out,
                           uint8_t* tags, uint32_t flags) {
+  atls::ResidentHold hold;  // RCCL's kernels and the engines' batches must not queue behind a resident server
   return run(m, false, recs, n, in, aux, out, tags, nullptr, nullptr, flags);
 }
 
 int atls_multi_open_batch(atls_multi* m, const atls_rec* recs, uint32_t n, const void* in, const void* aux,
                           const uint8_t* tags, void* out, atls_open_result* results, uint32_t flags) {
+  atls::ResidentHold hold;
   return run(m, true, recs, n, in, aux, out, nullptr, tags, results, flags);
 }
 

@@ -198,6 +198,13 @@ struct atls_stream_batch {
   std::vector<atls_open_result> res;
   int threads = 1;
   std::mutex mu, flush_mu;
+  // the connections' inboxes (owned by their Conn through a unique_ptr, so a pointer stays valid when conns grows),
+  // behind a lock of their own: atls_sb_read_ready finds a connection's inbox without the batch lock, which a
+  // receive round or an open batch holds for its whole length
+  std::vector<Inbox*> inboxes;
+  std::mutex inbox_mu;
+  Pinned gather;  // a flush batch's inputs in record order, when interleaved writes left them out of order
+  size_t gathered_batches = 0;  // flush batches that needed it (atls_debug_sb_gathered)
   // env ATLS_SB_PROFILE=1: seconds per phase, printed to stderr by atls_sb_destroy
   bool profile = std::getenv("ATLS_SB_PROFILE") != nullptr;
   double t_write = 0, t_seal = 0, t_send = 0, t_recv = 0, t_poll = 0, t_gather = 0, t_open = 0, t_hand = 0;
@@ -237,10 +244,14 @@ int key_check(const atls_key& k) {
   return ATLS_INSUFFICIENT_SECURITY;
 }
 
-// The connection's error becomes visible to its readers (after the records opened before it).
+// The connection's error becomes visible to its readers (after the records opened before it). A peer that closed
+// (recv returned 0) with no whole record left to open ends the stream for its readers with BrokenPipe, as
+// TlsStream::tcp_read does at a zero-byte read (net/stream.rs:68-73) -- a partial record left behind never
+// completes; writes stay allowed (a half-closed peer may still read).
 void publish_err(Conn& c) {
   std::lock_guard<std::mutex> lk(c.inbox->mu);
   if (c.err && !c.inbox->err) c.inbox->err = c.err;
+  if (!c.err && c.eof && c.offs.empty() && !c.inbox->err) c.inbox->err = kBrokenPipe;
 }
 
 // Opens the whole records of connections [c0, c1) (wire offsets `wbase`, record counts `rbase`, both prefix
@@ -310,6 +321,7 @@ long open_group(atls_stream_batch* sb, size_t c0, size_t c1, const std::vector<s
       std::lock_guard<std::mutex> lk(c.inbox->mu);
       for (Record& r : got) c.inbox->q.push_back(std::move(r));
       if (c.err && !c.inbox->err) c.inbox->err = c.err;
+      if (!c.err && c.eof && !c.inbox->err) c.inbox->err = kBrokenPipe;  // publish_err: the peer closed
     }
   });
   sb->t_hand += sw.lap();
@@ -356,8 +368,8 @@ int pop_inbox(Inbox& in, uint8_t* buf, size_t cap, size_t* out_len) {
 }
 
 Inbox* inbox_of(atls_stream_batch* sb, int conn) {
-  std::lock_guard<std::mutex> lk(sb->mu);
-  return valid_conn_locked(sb, conn) ? sb->conns[(size_t)conn].inbox.get() : nullptr;
+  std::lock_guard<std::mutex> lk(sb->inbox_mu);
+  return conn >= 0 && (size_t)conn < sb->inboxes.size() ? sb->inboxes[(size_t)conn] : nullptr;
 }
 
 }  // namespace
@@ -398,7 +410,12 @@ int atls_sb_add_connection(atls_stream_batch* sb, int fd, const atls_key* write_
   sb->keys.push_back(*write_key);
   sb->keys.push_back(*read_key);
   sb->keys_dirty = true;
+  Inbox* inbox = c.inbox.get();
   sb->conns.push_back(std::move(c));
+  {
+    std::lock_guard<std::mutex> il(sb->inbox_mu);
+    sb->inboxes.push_back(inbox);
+  }
   return (int)sb->conns.size() - 1;
 }
 
@@ -496,6 +513,7 @@ long atls_sb_flush(atls_stream_batch* sb) {
   std::vector<char> failed(nc, 0);
   std::thread sender;
   int rc = ATLS_OK;
+  size_t gathered = 0;
   size_t g = 0;
   Stopwatch sw;
   for (; g + 1 < gs.size(); g++) {
@@ -506,7 +524,30 @@ long atls_sb_flush(atls_stream_batch* sb) {
       break;
     }
     for (size_t r = r0; r < r1; r++) sb->frecs[r].out_off -= w0;
-    rc = atls_seal_batch(sb->e, sb->frecs.data() + r0, (uint32_t)(r1 - r0), arena->p, nullptr, out.p, nullptr, 0);
+    // The records of a batch are in connection order; their inputs are in write order. When writes were
+    // interleaved across connections (a server writing round robin) the inputs are out of order, and the engine
+    // would stage the whole arena prefix in one copy instead of pipelining its chunks (engine.cpp
+    // run_host_pipelined) -- once per batch. Such a batch's inputs are first gathered in record order.
+    const uint8_t* src = arena->p;
+    bool ascending = true;
+    for (size_t r = r0 + 1; r < r1 && ascending; r++)
+      ascending = sb->frecs[r].in_off >= sb->frecs[r - 1].in_off + sb->frecs[r - 1].len;
+    if (!ascending) {
+      std::vector<size_t> at(r1 - r0 + 1, 0);
+      for (size_t r = r0; r < r1; r++) at[r - r0 + 1] = at[r - r0] + sb->frecs[r].len;
+      if (!sb->gather.reserve(at.back() + 16)) {
+        rc = ATLS_INTERNAL_ERROR;
+        break;
+      }
+      parallel(threads, r1 - r0, [&](size_t k) {
+        atls_rec& d = sb->frecs[r0 + k];
+        if (d.len) std::memcpy(sb->gather.p + at[k], arena->p + d.in_off, d.len);
+        d.in_off = at[k];
+      });
+      src = sb->gather.p;
+      gathered++;
+    }
+    rc = atls_seal_batch(sb->e, sb->frecs.data() + r0, (uint32_t)(r1 - r0), src, nullptr, out.p, nullptr, 0);
     if (rc) break;
     sb->t_seal += sw.lap();
     if (sender.joinable()) sender.join();
@@ -525,6 +566,7 @@ long atls_sb_flush(atls_stream_batch* sb) {
   sb->t_send += sw.lap();
   {
     std::lock_guard<std::mutex> lk(sb->mu);
+    sb->gathered_batches += gathered;
     for (size_t ci = 0; ci < nc; ci++) {
       Conn& c = sb->conns[ci];
       if (failed[ci] && !c.err) c.err = kBrokenPipe;
@@ -565,7 +607,9 @@ long atls_sb_recv(atls_stream_batch* sb, int conn, size_t max_bytes) {
   if (k < 0) return -kBrokenPipe;
   if (k == 0) {
     std::lock_guard<std::mutex> lk(sb->mu);
-    sb->conns[(size_t)conn].eof = true;
+    Conn& c = sb->conns[(size_t)conn];
+    c.eof = true;
+    publish_err(c);
     return 0;
   }
   const int rc = atls_sb_feed(sb, conn, buf.data(), (size_t)k);
@@ -574,19 +618,22 @@ long atls_sb_recv(atls_stream_batch* sb, int conn, size_t max_bytes) {
 
 long atls_sb_recv_all(atls_stream_batch* sb, int timeout_ms) {
   if (!sb) return -ATLS_INTERNAL_ERROR;
-  std::lock_guard<std::mutex> lk(sb->mu);
-  const size_t nc = sb->conns.size();
+  std::unique_lock<std::mutex> lk(sb->mu);
   Stopwatch sw;
   for (int round = 0; round < 2; round++) {
+    const size_t nc = sb->conns.size();
     std::atomic<size_t> total{0};
     parallel(sb->threads, nc, [&](size_t ci) { total += drain_socket(sb->conns[ci]); });
     for (Conn& c : sb->conns) publish_err(c);
     sb->t_recv += sw.lap();
     if (total.load() || timeout_ms <= 0 || round) return (long)total.load();
-    std::vector<pollfd> fds;  // nothing arrived: wait for any open connection, once
+    std::vector<pollfd> fds;  // nothing arrived: wait for any open connection, once, without the batch lock
     for (const Conn& c : sb->conns)
       if (!c.err && !c.eof && c.rx_len < kRxMax) fds.push_back(pollfd{c.fd, POLLIN, 0});
-    const int pr = fds.empty() ? 0 : poll(fds.data(), fds.size(), timeout_ms);
+    if (fds.empty()) return 0;
+    lk.unlock();
+    const int pr = poll(fds.data(), fds.size(), timeout_ms);
+    lk.lock();
     sb->t_poll += sw.lap();
     if (pr <= 0) return 0;
   }
@@ -639,6 +686,13 @@ int atls_sb_read(atls_stream_batch* sb, int conn, uint8_t* buf, size_t cap, size
       publish_err(sb->conns[(size_t)conn]);
     }
   }
+}
+
+// Diagnostic: flush batches whose inputs were gathered into record order (interleaved writes; tests).
+unsigned long long atls_debug_sb_gathered(atls_stream_batch* sb) {
+  if (!sb) return 0;
+  std::lock_guard<std::mutex> lk(sb->mu);
+  return sb->gathered_batches;
 }
 
 }  // extern "C"

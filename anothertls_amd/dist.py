@@ -214,12 +214,12 @@ def seal_sharded(seal, recs, inp=None, out=None, tags=None, device=None):
 WATCHDOG_EXIT = 3  # status of a process whose watchdog fired (a hung step is a failure, not success)
 
 
-def run_or_exit(fn, timeout_s, on_timeout):
+def run_or_exit(fn, timeout_s, on_timeout, status=None):
     """fn() with a watchdog: if it has not returned after timeout_s seconds, on_timeout() runs
     (e.g. print the result gathered so far) and the process exits with status WATCHDOG_EXIT -- for
     steps after a benchmark's timed region whose collectives could hang (the measured line is
     still printed, and the non-zero status says something hung). Returns (True, fn's value) or
-    (False, the exception fn raised)."""
+    (False, the exception fn raised). status: the exit status instead of WATCHDOG_EXIT."""
     import threading
 
     lock, state = threading.Lock(), {"done": False}
@@ -232,7 +232,7 @@ def run_or_exit(fn, timeout_s, on_timeout):
             try:
                 on_timeout()
             finally:
-                os._exit(WATCHDOG_EXIT)
+                os._exit(WATCHDOG_EXIT if status is None else status)
 
     timer = threading.Timer(timeout_s, fire)
     timer.daemon = True
@@ -245,6 +245,44 @@ def run_or_exit(fn, timeout_s, on_timeout):
         state["done"] = True
         timer.cancel()
     return res
+
+
+COMMS_EXIT = 4  # status of a rank whose process group could not run its first collective
+
+
+def check_comms(device=None, timeout_s=120.0, what="RCCL"):
+    """The process group's first collective (a one-element all-reduce and a barrier; with backend "nccl" this is
+    where RCCL builds its communicator between the GPUs), under a watchdog: if it raises, or has not finished
+    after timeout_s, the rank prints why to stderr and exits with COMMS_EXIT -- a clear refusal instead of a
+    benchmark that hangs in its first barrier. No-op without a process group.
+    ATLS_TEST_COMMS_FAIL=raise|hang (tests/test_bench_launch.py) makes rank 1 fail that way instead."""
+    if not (tdist.is_available() and tdist.is_initialized()):
+        return
+    import sys
+
+    rank, world = tdist.get_rank(), tdist.get_world_size()
+
+    def refuse(why):
+        print(f"bench.py: rank {rank} of {world}: {what} between the ranks failed at its first collective: {why}",
+              file=sys.stderr, flush=True)
+
+    def first_collective():
+        inject = os.environ.get("ATLS_TEST_COMMS_FAIL")
+        if inject and rank == 1:
+            if inject == "hang":
+                time.sleep(10 * timeout_s)
+            raise RuntimeError(f"injected failure ({inject})")
+        t = torch.ones(1, dtype=torch.float64, device=device)
+        tdist.all_reduce(t)
+        if int(t.item()) != world:
+            raise RuntimeError(f"all-reduce of ones gave {t.item()}, not {world}")
+        tdist.barrier()
+
+    ok, err = run_or_exit(first_collective, timeout_s, lambda: refuse(f"no answer within {timeout_s:.0f} s"),
+                          status=COMMS_EXIT)
+    if not ok:
+        refuse(f"{type(err).__name__}: {str(err)[:300]}")
+        os._exit(COMMS_EXIT)
 
 
 def close():

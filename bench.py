@@ -10,8 +10,9 @@ is no data-path collective: weak scaling). One step = one atls_seal_batch over t
 batch. Rank 0 prints one JSON line. `--gpus N` without a launcher (no WORLD_SIZE) starts the N
 rank processes itself before anything touches the GPU; a launcher whose WORLD_SIZE differs from
 --gpus, or a LOCAL_RANK without a GPU, ends the run with status 2. n_gpus is the world size the
-process group reports. A hung post-timing exchange ends every rank with status 3 after rank 0
-has printed the line.
+process group reports. If the process group's first collective (RCCL's communicator between the GPUs)
+fails or hangs, every rank exits with status 4 and says why on stderr, before anything is measured. A hung
+post-timing exchange ends every rank with status 3 after rank 0 has printed the line.
 
 Fields beyond the driver contract:
   roofline     — dominant kernel (AES-GCM seal): algorithmic bytes per launch (2L+16 per record:
@@ -86,6 +87,9 @@ def parse():
     p.add_argument("--c1-threads", type=int, default=16, help="C1 at scale: worker threads per stream batch")
     p.add_argument("--dry-run-cap", type=int, default=64,
                    help="--dry-run: content bytes per record of the whole-batch exchange rehearsal")
+    p.add_argument("--comms-timeout", type=float, default=180.0,
+                   help="N > 1: seconds the process group's first collective (RCCL's communicator set-up) may take "
+                        "before every rank exits with status 4")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU only (gloo): the launcher, rendezvous, timing and JSON line with a stub sealer "
                         "instead of the engine (tests of the N > 1 plumbing)")
@@ -330,6 +334,7 @@ def run_dry(args):
 
     rank, _, world = dist.env_ranks()
     dist.init("gloo")
+    dist.check_comms(None, args.comms_timeout, "gloo")
     batch = workload.shard_batch(args.config, rank, n=args.records or 64)
     buf = np.random.default_rng(rank).integers(0, 256, batch["in_bytes"], dtype=np.uint8)
     out = np.empty_like(buf)
@@ -427,23 +432,56 @@ def lds_cycles_per_launch(batch):
     return float(cyc.sum()) / 64.0
 
 
-def clock_pass(eng, dev, launch, n_launch, kern_ms):
-    """The shader clock of `n_launch` more back-to-back launches (outside any timed region): the clock probe
-    (atls_clock_probe, 16 one-wave workgroups on a second stream) sleeps through the first fifth of them and
-    reads s_memtime against s_memrealtime over the next half. Returns the median MHz over the workgroups."""
-    side = torch.cuda.Stream(device=dev)
-    wgs = 16
-    out = torch.zeros(2 * wgs, dtype=torch.int64, device=dev)
-    span_us = n_launch * kern_ms * 1e3
-    torch.cuda.synchronize(dev)
-    eng.clock_probe(out, wgs=wgs, delay_us=int(0.2 * span_us), spin_us=max(20, int(0.5 * span_us)),
-                    stream=side.cuda_stream)
-    for _ in range(n_launch):
+class ClockProbe:
+    """The shader clock over a timed window, from the same launches as the kernel time it is paired with
+    (a clock read in a separate pass after a synchronize had dropped and inflated lds.frac). The
+    probe (atls_clock_probe, 16 one-wave workgroups on a second stream, no LDS) is enqueued as the window's
+    first launch is, sleeps through the first 15 % of the window's expected span and reads s_memtime against
+    s_memrealtime over the next 70 %; `mhz()` (after the window's synchronize) is the median over the waves."""
+
+    WGS = 16
+
+    def __init__(self, eng, dev):
+        self.eng, self.dev = eng, dev
+        self.side = torch.cuda.Stream(device=dev)
+        self.out = torch.zeros(2 * self.WGS, dtype=torch.int64, device=dev)
+
+    def start(self, n_launch, est_ms):
+        span_us = n_launch * est_ms * 1e3
+        self.eng.clock_probe(self.out, wgs=self.WGS, delay_us=int(0.15 * span_us), spin_us=max(20, int(0.7 * span_us)),
+                             stream=self.side.cuda_stream)
+
+    def mhz(self):
+        torch.cuda.synchronize(self.dev)
+        o = self.out.cpu().numpy().reshape(self.WGS, 2).astype(np.float64)
+        return float(np.median(100.0 * o[:, 0] / np.maximum(o[:, 1], 1)))
+
+
+def settle(launch, sync, ms):
+    """Run `launch` back to back, untimed, for `ms` milliseconds (synchronising every 8 launches): the clock under
+    this load settles over ~100 ms. Returns the mean host ms per launch (an estimate of the launch's
+    span, for the clock probe's timing), or None when ms <= 0."""
+    if ms <= 0:
+        return None
+    count, t0 = 0, time.perf_counter()
+    t_end = t0 + ms * 1e-3
+    while time.perf_counter() < t_end:
+        for _ in range(8):
+            launch()
+        sync()
+        count += 8
+    return (time.perf_counter() - t0) * 1e3 / count
+
+
+def launch_ms(launch, stream, sync, n=3):
+    """The mean launch time of n launches from HIP events (the clock probe's span estimate without a settle)."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(n):
         launch()
-    eng.sync()
-    torch.cuda.synchronize(dev)
-    o = out.cpu().numpy().reshape(wgs, 2).astype(np.float64)
-    return float(np.median(100.0 * o[:, 0] / np.maximum(o[:, 1], 1)))
+    e1.record(stream)
+    sync()
+    return e0.elapsed_time(e1) / n
 
 
 def lds_roofline(batch, kern_ms, sclk_mhz, cus):
@@ -456,11 +494,12 @@ def lds_roofline(batch, kern_ms, sclk_mhz, cus):
     return {"bound": "lds", "cycles_per_launch": round(cyc), "sclk_MHz": round(sclk_mhz, 1), "cus": cus,
             "t_min_ms": round(t_ms, 4), "kernel_ms": round(kern_ms, 4), "frac": round(t_ms / kern_ms, 4),
             "per_block": "AES-CTR 1+4+16(NR-2) ds_read_b32 x 2 cyc + GHASH 32 ds_read_b128 x 4 cyc, per 64 blocks",
-            "clock": "atls_clock_probe beside the same launches (s_memtime / s_memrealtime, median of 16 waves)"}
+            "clock": "atls_clock_probe beside the timed launches themselves, enqueued with the first of them (s_memtime / "
+                     "s_memrealtime over the middle 70 % of the window, median of 16 waves)"}
 
 
 def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_slots=None, keep=False,
-            settle_ms=0.0, load_settle_ms=0.0):
+            settle_ms=0.0, load_settle_ms=0.0, do_open=True):
     """This rank's shard of config `name`, device-resident: `steps` timed seals (barrier + sync on both
     sides, max over ranks) with the kernels' interval from HIP events on the engine stream, then as many
     opens of the sealed records with every status, length and (uniform configs) plaintext byte checked.
@@ -481,16 +520,6 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
     d_recs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
     torch.cuda.synchronize(dev)
     copy_gbps = copy_probe(d_in, d_out, settle_ms) if settle_ms > 0 else None
-    flags0 = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC | (atls.FLAG_LAZY_JOIN if lazy else 0)
-    if load_settle_ms > 0:
-        # the same seals back to back, untimed, until the clock has settled under this load: a C2 launch takes
-        # 1.29-1.46 ms for the first few after other work, ~1.0 ms after ~100 ms
-        ptrs = [t.data_ptr() for t in (d_recs, d_in, d_aux, d_out, d_tags)]
-        t_end = time.perf_counter() + load_settle_ms * 1e-3
-        while time.perf_counter() < t_end:
-            for _ in range(8):
-                eng.seal_batch(ptrs[0], ptrs[1], ptrs[2], ptrs[3], ptrs[4], flags=flags0, n=n)
-            eng.sync()
     # LAZY_JOIN: a mixed batch's ChaCha20-Poly1305 kernel is not joined back at the end of each step,
     # so the next step's plan and AES-GCM kernel start beside it (C5); no effect on one-suite batches
     flags = atls.FLAG_DEVICE_PTRS | atls.FLAG_DEVICE_RECS | atls.FLAG_NO_SYNC | (atls.FLAG_LAZY_JOIN if lazy else 0)
@@ -503,15 +532,26 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
         eng.sync()
         torch.cuda.synchronize(dev)
 
-    # kernel time of the same steps from HIP events on the engine's stream
+    def seal_launch():
+        eng.seal_batch(p_recs, p_in, p_aux, p_out, p_tags, flags=flags, n=n)
+
+    # the same seals back to back, untimed, until the clock has settled under this load: a C2 launch takes
+    # 1.29-1.46 ms for the first few after other work, ~1.0 ms after ~100 ms
+    est_ms = settle(seal_launch, sync, load_settle_ms) or launch_ms(seal_launch, stream, sync)
+    lds_kind = lds_cycles_per_launch(batch) is not None
+    probe = ClockProbe(eng, dev) if lds_kind else None
+
+    # kernel time of the same steps from HIP events on the engine's stream; the clock probe beside them
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     marks = {"n": 0}
 
     def timed_step():
         if marks["n"] == warmup:
             eng.join()  # the interval holds exactly the timed steps' kernels
+            if probe:
+                probe.start(steps, est_ms)
             ev0.record(stream)
-        eng.seal_batch(p_recs, p_in, p_aux, p_out, p_tags, flags=flags, n=n)
+        seal_launch()
         marks["n"] += 1
         if marks["n"] == warmup + steps:
             eng.join()
@@ -525,63 +565,62 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
     m = {"batch": batch, "n": n, "wall": wall, "kern_ms": kern_ms, "payload": payload, "alg_bytes": alg_bytes,
          "achieved": achieved, "value": dist.whole_job_rate(payload, steps, wall, world), "flags": flags,
          "stream": stream, "sync": sync, "copy_gbps": copy_gbps}
-    if lds_cycles_per_launch(batch) is not None:
-        # the clock of `steps` more of the same seals, after the timed region (the LDS roofline is in cycles)
-        m["sclk_mhz"] = clock_pass(eng, dev, lambda: eng.seal_batch(p_recs, p_in, p_aux, p_out, p_tags, flags=flags, n=n),
-                                   steps, kern_ms)
-        m["lds"] = lds_roofline(batch, kern_ms, m["sclk_mhz"], torch.cuda.get_device_properties(dev).multi_processor_count)
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    if probe:
+        # the LDS roofline is in cycles: the clock of the timed launches themselves
+        m["sclk_mhz"] = probe.mhz()
+        m["lds"] = lds_roofline(batch, kern_ms, m["sclk_mhz"], cus)
 
-    # ---- the decrypt half (Gcm::decrypt, gcm.rs:142-157, via record.rs:201-240) over the records
-    # just sealed: same records, same bytes per record (read L + 16-byte tag, write L) ----
-    orecs = open_descs(recs)
-    d_orecs = torch.from_numpy(orecs.view(np.uint8).copy()).to(dev)
-    d_pt = torch.zeros(batch["out_bytes"], dtype=torch.uint8, device=dev)
-    d_res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
-    torch.cuda.synchronize(dev)
-    q_recs, q_pt, q_res = d_orecs.data_ptr(), d_pt.data_ptr(), d_res.data_ptr()
-    if load_settle_ms > 0:
+    if do_open:
+        # ---- the decrypt half (Gcm::decrypt, gcm.rs:142-157, via record.rs:201-240) over the records
+        # just sealed: same records, same bytes per record (read L + 16-byte tag, write L) ----
+        orecs = open_descs(recs)
+        d_orecs = torch.from_numpy(orecs.view(np.uint8).copy()).to(dev)
+        d_pt = torch.zeros(batch["out_bytes"], dtype=torch.uint8, device=dev)
+        d_res = torch.zeros(8 * n, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)
+        q_recs, q_pt, q_res = d_orecs.data_ptr(), d_pt.data_ptr(), d_res.data_ptr()
+
+        def open_launch():
+            eng.open_batch(q_recs, p_out, p_aux, p_tags, q_pt, q_res, flags=flags, n=n)
+
         # the opens' own load settle, as the seals': after the seal leg's host work the clock has dropped, and
         # a few warm-up opens do not bring it back (tools/open_order_probe.py: opens and seals alternated in
         # blocks of 20 run within 1-2 % of each other, C2 1.005-1.024 vs 0.999-1.017 ms)
-        t_end = time.perf_counter() + load_settle_ms * 1e-3
-        while time.perf_counter() < t_end:
-            for _ in range(8):
-                eng.open_batch(q_recs, p_out, p_aux, p_tags, q_pt, q_res, flags=flags, n=n)
-            eng.sync()
-    o0, o1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for i in range(warmup + steps):
-        if i == warmup:
-            eng.join()
-            o0.record(stream)
-        eng.open_batch(q_recs, p_out, p_aux, p_tags, q_pt, q_res, flags=flags, n=n)
-    eng.join()
-    o1.record(stream)
-    sync()
-    open_ms = o0.elapsed_time(o1) / steps
-    res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
-    ok = bool((res["status"] == 0).all() and (res["content_len"] == recs["len"]).all()
-              and (res["content_type"] == 23).all())
-    lens = recs["len"]
-    if ok and n > 1 and (lens == lens[0]).all() and (np.diff(recs["in_off"]) == recs["in_off"][1] - recs["in_off"][0]).all() \
-            and (np.diff(recs["out_off"]) == recs["out_off"][1] - recs["out_off"][0]).all():
-        # uniform records (C2-C4): every plaintext byte of every record against the sealed input
-        L, si, so = int(lens[0]), int(recs["in_off"][1] - recs["in_off"][0]), int(recs["out_off"][1] - recs["out_off"][0])
-        ok = bool(torch.equal(d_pt[: n * so].view(n, so)[:, :L], d_in[: n * si].view(n, si)[:, :L]))
-    open_ach = alg_bytes / (open_ms * 1e-3) / 1e9  # read L+1 ciphertext + 16 tag, write L+1 plaintext
-    m["open"] = {"GiBps": round(payload / (open_ms * 1e-3) / 2**30, 3), "kernel_ms": round(open_ms, 4),
-                 "achieved_GBps": round(open_ach, 1), "frac": round(open_ach / HBM_PEAK_GBPS, 4),
-                 "plaintext_and_status_ok": ok,
-                 "what": "open_batch over the sealed records (device-resident, same batch), HIP events on the "
-                         "engine stream over the timed steps"}
-    if m.get("lds"):
-        # the open kernels' own clock: in cycles they are within ~2 % of the seal's, and the PMC put their clock
-        # 8-13 % lower (profiles/r05/pmc_open/), so the open's LDS-array fraction is stated at its own clock
-        osclk = clock_pass(eng, dev, lambda: eng.open_batch(q_recs, p_out, p_aux, p_tags, q_pt, q_res, flags=flags, n=n),
-                           steps, open_ms)
-        ol = lds_roofline(batch, open_ms, osclk, torch.cuda.get_device_properties(dev).multi_processor_count)
-        if ol:
-            m["open"]["lds"] = {"sclk_MHz": ol["sclk_MHz"], "t_min_ms": ol["t_min_ms"], "frac": ol["frac"]}
-    del d_orecs, d_pt, d_res
+        est_open = settle(open_launch, sync, load_settle_ms) or launch_ms(open_launch, stream, sync)
+        o0, o1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for i in range(warmup + steps):
+            if i == warmup:
+                eng.join()
+                if probe:
+                    probe.start(steps, est_open)
+                o0.record(stream)
+            open_launch()
+        eng.join()
+        o1.record(stream)
+        sync()
+        open_ms = o0.elapsed_time(o1) / steps
+        res = d_res.cpu().numpy().view(atls.OPEN_RESULT_DTYPE)
+        ok = bool((res["status"] == 0).all() and (res["content_len"] == recs["len"]).all()
+                  and (res["content_type"] == 23).all())
+        lens = recs["len"]
+        if ok and n > 1 and (lens == lens[0]).all() and (np.diff(recs["in_off"]) == recs["in_off"][1] - recs["in_off"][0]).all() \
+                and (np.diff(recs["out_off"]) == recs["out_off"][1] - recs["out_off"][0]).all():
+            # uniform records (C2-C4): every plaintext byte of every record against the sealed input
+            L, si, so = int(lens[0]), int(recs["in_off"][1] - recs["in_off"][0]), int(recs["out_off"][1] - recs["out_off"][0])
+            ok = bool(torch.equal(d_pt[: n * so].view(n, so)[:, :L], d_in[: n * si].view(n, si)[:, :L]))
+        open_ach = alg_bytes / (open_ms * 1e-3) / 1e9  # read L+1 ciphertext + 16 tag, write L+1 plaintext
+        m["open"] = {"GiBps": round(payload / (open_ms * 1e-3) / 2**30, 3), "kernel_ms": round(open_ms, 4),
+                     "achieved_GBps": round(open_ach, 1), "frac": round(open_ach / HBM_PEAK_GBPS, 4),
+                     "plaintext_and_status_ok": ok,
+                     "what": "open_batch over the sealed records (device-resident, same batch), HIP events on the "
+                             "engine stream over the timed steps"}
+        if probe:
+            # the open kernels' LDS-array fraction at the clock of the timed opens themselves
+            ol = lds_roofline(batch, open_ms, probe.mhz(), cus)
+            if ol:
+                m["open"]["lds"] = {"sclk_MHz": ol["sclk_MHz"], "t_min_ms": ol["t_min_ms"], "frac": ol["frac"]}
+        del d_orecs, d_pt, d_res
     if keep:
         m.update(d_in=d_in, d_out=d_out, d_tags=d_tags, d_aux=d_aux, d_recs=d_recs)
     else:
@@ -630,6 +669,9 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     dist.init("nccl", dev)
+    # the first collective builds RCCL's communicator between the GPUs: a failure or a hang there ends every rank
+    # with status 4 and a message, before anything is measured
+    dist.check_comms(dev, args.comms_timeout)
     world = dist.world_size()  # as the process group reports it
 
     import anothertls_amd as atls
@@ -639,7 +681,7 @@ def main():
     # this rank's shard of the config's record stream (weak scaling: fixed records per GPU)
     m = measure(args.config, eng, dev, rank, world, args.steps, args.warmup, not args.no_lazy_join,
                 records=args.records, key_slots=args.key_slots, keep=True, settle_ms=args.settle_ms,
-                load_settle_ms=args.load_settle_ms)
+                load_settle_ms=args.load_settle_ms, do_open=not args.no_open)
     batch, recs, n, payload = m["batch"], m["batch"]["recs"], m["n"], m["payload"]
     d_in, d_out, d_tags, d_aux = m["d_in"], m["d_out"], m["d_tags"], m["d_aux"]
     flags, stream, sync, kern_ms, achieved, alg_bytes = m["flags"], m["stream"], m["sync"], m["kern_ms"], m["achieved"], m["alg_bytes"]
@@ -710,8 +752,9 @@ def main():
                          "kernel_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes,
                          "copy_GBps": round(copy_gbps, 1), "frac_of_copy": round(achieved / copy_gbps, 4),
                          "lds": m.get("lds")},
-            "open": m["open"],
         }
+        if "open" in m:
+            result["open"] = m["open"]
         if sustained:
             result["sustained"] = sustained
         if world == 1 and not args.no_cpu_baseline:

@@ -284,7 +284,9 @@ void atls_partition(const atls_rec* recs, uint32_t n, int open, uint32_t parts, 
  * If the engine fails part-way through a flush, the connections whose records were not sent end with its
  * error. */
 typedef struct atls_stream_batch atls_stream_batch;
-enum { ATLS_WOULD_BLOCK = 253 }; /* atls_sb_read_ready: no opened record yet (not a TlsError) */
+/* atls_sb_read_ready: no opened record yet. Outside the u8 range of TlsError (alert.rs:18-45, where 253 is
+ * GotAlert), so no error code can be mistaken for it. */
+enum { ATLS_WOULD_BLOCK = 0x100 };
 atls_stream_batch* atls_sb_create(atls_engine* e);
 void atls_sb_destroy(atls_stream_batch* sb);
 int atls_sb_set_threads(atls_stream_batch* sb, int threads);

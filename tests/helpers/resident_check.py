@@ -4,7 +4,8 @@ it; =2: AES-GCM calls too, gcm.hip single_resident<true>) against the oracle: Ch
 (chacha20/cipher.rs:99-102) and the argument-block limit; AES-128/-192/-256-GCM (gcm.rs:42-162) with 12-byte
 and other IVs; AADs of 0-40 bytes; seal / open / tampered tag; suites interleaved; batch launches between
 calls (the server steps aside and comes back, building its AES tables again); calls after the server left on
-its idle timeout; and 8 threads at once."""
+its idle timeout; 8 threads at once; and 8 threads of calls without a pause beside a thread sealing batches,
+each batch within a bound (VERDICT r5 weak #4)."""
 import os
 import random
 import sys
@@ -104,7 +105,77 @@ def main():
     for th in ths:
         th.join(120)
     assert not errors, errors[:2]
+    print("8 threads OK", flush=True)
+    batches_beside_calls(ciphers, keys)
     print("resident OK")
+
+
+def batches_beside_calls(ciphers, keys, n_batches=40, bound_s=1.0):
+    """8 threads of single calls through the server without a pause while another thread seals
+    batches on its own engine. Every batch must finish within bound_s (a batch enqueued behind a server kept
+    alive by the calls would wait until they stop), equal the first batch byte for byte, which equals the oracle
+    (crypto/aes/gcm.rs:42-162 via net/record.rs:162-198); every call is checked against the oracle by one()."""
+    import ctypes
+
+    from anothertls_amd import workload
+    eng = atls.Engine(0)
+    b = workload.tls_batch(256, 16384, AES128, n_keys=8)
+    recs = b["recs"]
+    eng.set_keys(b["keys"])
+    h_in = np.random.default_rng(7).integers(0, 256, b["in_bytes"] + 16, dtype=np.uint8)
+    aux = np.zeros(16, np.uint8)
+    ref_out, ref_tags = np.zeros(b["out_bytes"] + 16, np.uint8), np.zeros(16 * len(recs), np.uint8)
+    eng.seal_batch(recs, h_in, aux, ref_out, ref_tags)
+    o_out, o_tags = np.zeros_like(ref_out), np.zeros_like(ref_tags)
+    okeys = (ora.OraKey * len(b["keys"])).from_buffer_copy(b["keys"].tobytes())
+    orecs = (ora.OraRec * len(recs)).from_buffer_copy(recs.tobytes())
+    ora.seal_batch(okeys, orecs, h_in, aux, o_out, o_tags, 8)
+    assert np.array_equal(ref_out, o_out) and np.array_equal(ref_tags, o_tags), "batch != oracle"
+    lib = atls.library()
+    lib.atls_debug_resident_fallbacks.restype = ctypes.c_ulonglong
+    fb0 = lib.atls_debug_resident_fallbacks()
+    stop, errors, calls, times = threading.Event(), [], [0] * 8, []
+
+    def caller(t):
+        r = random.Random(100 + t)
+        t_end = time.monotonic() + 60.0
+        try:
+            while not stop.is_set() and time.monotonic() < t_end:
+                s = (CHACHA, AES128, AES256)[(t + calls[t]) % 3]
+                one(ciphers, r, s, keys[s][calls[t] % 3], r.choice([0, 17, 700, 1537, 3000]), r.choice([0, 5]))
+                calls[t] += 1
+        except BaseException as ex:  # noqa: BLE001
+            errors.append(ex)
+
+    def batcher():
+        try:
+            out, tags = np.zeros_like(ref_out), np.zeros_like(ref_tags)
+            time.sleep(0.2)  # the callers are running
+            for _ in range(n_batches):
+                out[:] = 0
+                t0 = time.perf_counter()
+                eng.seal_batch(recs, h_in, aux, out, tags)
+                times.append(time.perf_counter() - t0)
+                assert np.array_equal(out, ref_out) and np.array_equal(tags, ref_tags), "batch beside calls differs"
+        except BaseException as ex:  # noqa: BLE001
+            errors.append(ex)
+        finally:
+            stop.set()
+
+    ths = [threading.Thread(target=caller, args=(t,)) for t in range(8)] + [threading.Thread(target=batcher)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(120)
+    eng.close()
+    assert not errors, errors[:2]
+    assert len(times) == n_batches, times
+    fb = lib.atls_debug_resident_fallbacks() - fb0
+    print(f"batches beside calls: {n_batches} batches, max {max(times) * 1e3:.1f} ms, median "
+          f"{sorted(times)[len(times) // 2] * 1e3:.1f} ms; {sum(calls)} calls, {fb} of them launched while a batch "
+          f"held the server", flush=True)
+    assert max(times) < bound_s, times
+    assert sum(calls) > 8 * 10, calls
 
 
 if __name__ == "__main__":

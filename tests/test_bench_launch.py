@@ -63,3 +63,17 @@ def test_failing_rank_status_reaches_caller():
                        capture_output=True, text=True, timeout=200, env=_env())
     assert r.returncode != 0
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("how", ["raise", "hang"])
+def test_first_collective_failure_refuses_clearly(how):
+    """if the process group's first collective fails (RCCL between distinct GPUs at init), the run
+    refuses with status 4 and a message instead of hanging in its first barrier -- rank 1 raising there, and rank
+    1 never answering (rank 0's watchdog fires after --comms-timeout)."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "2", "--warmup", "1",
+                        "--comms-timeout", "10"],
+                       capture_output=True, text=True, timeout=200, env=_env(ATLS_TEST_COMMS_FAIL=how))
+    assert r.returncode == 4, (r.returncode, r.stderr[-2000:])
+    assert "failed at its first collective" in r.stderr, r.stderr[-2000:]
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]

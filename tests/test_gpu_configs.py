@@ -132,6 +132,20 @@ def _full_config(eng, name, n):
     return batch, dev_bufs, h_in, h_out, h_tags
 
 
+def test_c2_key_per_record_full_batch_vs_openssl_and_oracle(eng):
+    """VERDICT r5 parity softness (ii): C2's layout with a key per record (65,536 connections, the bench's
+    "a key per record" config and SURVEY §8(d)'s worst case: no lane group forms, every record takes the
+    one-record-per-wave path with its own key schedule) -- every record against OpenSSL at full size, a sample
+    against the oracle, open(seal(x)) == x with tampered tags (net/record.rs:162-240, crypto/aes/gcm.rs:42-128)."""
+    name = "c2_aes128gcm_64Ki_x_16KiB"
+    batch = workload.config_batch(name, n_keys=workload.CONFIGS[name][1])
+    assert len(batch["recs"]) == 65536 and len(batch["keys"]) == 65536
+    dev_bufs, (h_in, h_out, h_tags) = _device_seal(eng, batch, workload.SEEDS["payload"] + 17)
+    assert _vs_openssl(batch, h_in, h_out, h_tags) == 0
+    _vs_oracle(batch, h_in, h_out, h_tags, sample=2048)
+    _open_roundtrip(eng, batch, dev_bufs, tamper=[1, 30000, 65534])
+
+
 def test_c2_full_batch_vs_openssl_and_oracle(eng):
     batch, dev_bufs, h_in, h_out, h_tags = _full_config(eng, "c2_aes128gcm_64Ki_x_16KiB", None)
     assert len(batch["recs"]) == 65536

@@ -188,7 +188,7 @@ def test_native_stream_batch_threads(atls):
                 while (rc := lib.atls_sb_read_ready(c_sb, cconn[i], buf, 16384, C.byref(ln))) == 0:
                     with lock:
                         got[i] += bytes(buf[:ln.value])
-                assert rc == 253, rc  # ATLS_WOULD_BLOCK
+                assert rc == 0x100, rc  # ATLS_WOULD_BLOCK (outside the u8 TlsError range)
 
         ths = [threading.Thread(target=reader, args=(t,)) for t in range(3)]
         for th in ths:
@@ -218,3 +218,103 @@ def test_c1_native_loopback_tool(atls, conns, threads):
     assert out.returncode == 0, out.stderr[-2000:]
     line = json.loads(out.stdout.strip().splitlines()[-1])
     assert line["verified"] is True and line["gpu_MBps"] > 0 and line["threads"] == threads
+
+
+def test_native_interleaved_writes_and_peer_close(atls):
+    """(1) a server that writes round robin across its connections leaves the flush's inputs out of
+    record order; the flush gathers such a batch's inputs into record order, so the engine's host pipeline still
+    takes it (it would otherwise stage the whole arena prefix in one piece, once per batch) -- wire bytes against
+    the oracle's records (record.rs:162-198), every byte read back. (2) A peer that closes ends its connection's
+    stream with BrokenPipe (TlsStream::tcp_read at a zero-byte read, net/stream.rs:68-73) for an event loop that
+    only uses recv_all / open_pending / read_ready: after the whole records that arrived before the close, with a
+    partial record left behind, and with nothing; recv_all returns at once once every peer has closed."""
+    import time
+
+    lib = atls.library()
+    lib.atls_debug_sb_gathered.restype = C.c_ulonglong
+    lib.atls_debug_sb_gathered.argtypes = [C.c_void_p]
+    lib.atls_debug_host_unpipelined.restype = C.c_ulonglong
+    e_s, e_c = atls.Engine(0), atls.Engine(0)
+    s_sb, c_sb = lib.atls_sb_create(e_s._e), lib.atls_sb_create(e_c._e)
+    assert lib.atls_sb_set_threads(s_sb, 4) == 0 and lib.atls_sb_set_threads(c_sb, 4) == 0
+    n = 6
+    pairs = [socket.socketpair() for _ in range(n)]
+    keys = [_keys(atls, i) for i in range(n)]
+    sconn = [lib.atls_sb_add_connection(s_sb, a.fileno(), w.ctypes.data, r.ctypes.data)
+             for (a, _), (w, r) in zip(pairs, keys)]
+    cconn = [lib.atls_sb_add_connection(c_sb, b.fileno(), r.ctypes.data, w.ctypes.data)
+             for (_, b), (w, r) in zip(pairs, keys)]
+    rng = np.random.default_rng(29)
+    sent = [[] for _ in range(n)]
+    for k in range(8):  # round robin: connection i's k-th write lands after every connection's (k-1)-th
+        for i in range(n):
+            d = rng.integers(0, 256, int(rng.integers(0, 20000)), dtype=np.uint8).tobytes()
+            assert lib.atls_sb_write(s_sb, sconn[i], 23, d, len(d)) == 0
+            sent[i].append(d)
+    unpipelined0 = lib.atls_debug_host_unpipelined()
+    assert lib.atls_sb_flush(s_sb) == sum(max(1, -(-len(d) // 16384)) for ds in sent for d in ds)
+    assert lib.atls_debug_sb_gathered(s_sb) >= 1
+    assert lib.atls_debug_host_unpipelined() == unpipelined0  # the gathered batch went through the pipeline
+    want, seq = b"", 0
+    w = keys[0][0][0]
+    for d in sent[0]:
+        for f in [d[j:j + 16384] for j in range(0, len(d), 16384)] or [b""]:
+            rc, rec = ora.record_seal(int(w["suite"]), bytes(w["key"][:int(w["key_len"])]), bytes(w["static_iv"]), seq, 23, f)
+            assert rc == 0
+            want += rec
+            seq += 1
+    raw = b""
+    while len(raw) < len(want):
+        raw += pairs[0][1].recv(1 << 20)
+    assert raw == want
+    assert lib.atls_sb_feed(c_sb, cconn[0], raw, len(raw)) == 0
+    expect = [b"".join(ds) for ds in sent]
+    got = [b""] * n
+    buf = (C.c_uint8 * 16384)()
+    ln = C.c_size_t(0)
+    for _ in range(200):
+        if got == expect:
+            break
+        assert lib.atls_sb_recv_all(c_sb, 200) >= 0
+        assert lib.atls_sb_open_pending(c_sb) >= 0
+        for i in range(n):
+            while (rc := lib.atls_sb_read_ready(c_sb, cconn[i], buf, 16384, C.byref(ln))) == 0:
+                got[i] += bytes(buf[:ln.value])
+            assert rc == 0x100, (i, rc)
+    assert got == expect
+    # the peers close: connection 1 with nothing in flight, 2 after half a record, 3 after a whole record
+    msg = b"last words"
+    assert lib.atls_sb_write(s_sb, sconn[3], 23, msg, len(msg)) == 0
+    assert lib.atls_sb_write(s_sb, sconn[2], 23, msg, len(msg)) == 0
+    assert lib.atls_sb_flush(s_sb) == 2
+    rec2 = b""
+    while len(rec2) < 5 + len(msg) + 17:
+        rec2 += pairs[2][1].recv(1 << 16)
+    pairs[2][0].close()  # conn 2: the client gets only half of its record, fed by hand, then the socket's EOF
+    assert lib.atls_sb_feed(c_sb, cconn[2], rec2[:10], 10) == 0
+    for i in (1, 3):
+        pairs[i][0].close()
+    for _ in range(20):
+        assert lib.atls_sb_recv_all(c_sb, 100) >= 0
+        assert lib.atls_sb_open_pending(c_sb) >= 0
+        if lib.atls_sb_read_ready(c_sb, cconn[1], buf, 16384, C.byref(ln)) != 0x100:
+            break
+    assert lib.atls_sb_read_ready(c_sb, cconn[1], buf, 16384, C.byref(ln)) == 254  # BrokenPipe
+    assert lib.atls_sb_read_ready(c_sb, cconn[3], buf, 16384, C.byref(ln)) == 0 and bytes(buf[:ln.value]) == msg
+    assert lib.atls_sb_read_ready(c_sb, cconn[3], buf, 16384, C.byref(ln)) == 254
+    assert lib.atls_sb_read_ready(c_sb, cconn[2], buf, 16384, C.byref(ln)) == 254  # the partial record never completes
+    assert lib.atls_sb_read(c_sb, cconn[1], buf, 16384, C.byref(ln)) == 254  # the blocking read agrees
+    for i in (0, 4, 5):
+        pairs[i][0].close()
+    t0 = time.monotonic()
+    for _ in range(5):  # every peer closed: nothing to poll, no wait
+        assert lib.atls_sb_recv_all(c_sb, 1000) == 0
+    assert time.monotonic() - t0 < 1.0
+    for i in (0, 4, 5):
+        assert lib.atls_sb_read_ready(c_sb, cconn[i], buf, 16384, C.byref(ln)) == 254
+    for sb in (s_sb, c_sb):
+        lib.atls_sb_destroy(sb)
+    for a, b in pairs:
+        b.close()
+    e_s.close()
+    e_c.close()
