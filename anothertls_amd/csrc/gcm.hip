@@ -1139,8 +1139,16 @@ __device__ unsigned long long g_clk_stamps[4];
 template <bool OPEN, int kWaves, int NR>
 __device__ __forceinline__ void gcm_kernel_body(const GcmArgs& A);
 
+// ATLS_GCM_MINW: minimum waves per SIMD of the 12-wave record kernels (__launch_bounds__): 4 caps them at 128
+// VGPRs, so that in a mixed batch a 128-VGPR ChaCha20-Poly1305 wave (chacha_kernel<*, true>) still fits on each
+// SIMD beside the workgroup's three AES-GCM waves (3 x 128 + 128 = 512). The seal kernel had grown to 129
+// VGPRs (136 allocated: 3 x 136 + 128 > 512), which kept the two kernels of a C5 seal off each other's CUs.
+// AES-192 keeps the 168 cap (at 128 its open kernel spills; no mixed config uses it).
+#ifndef ATLS_GCM_MINW
+#define ATLS_GCM_MINW 4
+#endif
 template <bool OPEN, int kWaves, int NR>
-__global__ __launch_bounds__(64 * kWaves) void gcm_kernel(GcmArgs A) {
+__global__ __launch_bounds__(64 * kWaves, (kWaves == 12 && NR != 12) ? ATLS_GCM_MINW : 1) void gcm_kernel(GcmArgs A) {
 #ifdef ATLS_CLK_STAMPS
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   gcm_kernel_body<OPEN, kWaves, NR>(A);

@@ -445,6 +445,11 @@ class ClockProbe:
         self.eng, self.dev = eng, dev
         self.side = torch.cuda.Stream(device=dev)
         self.out = torch.zeros(2 * self.WGS, dtype=torch.int64, device=dev)
+        # one probe launch here, before any timed window: the first launch of a kernel loads its code object
+        # (milliseconds with the host blocked and the GPU idle), which inside the window left the GPU idle and
+        # its clock falling (profiles/r06/first/: C2's window at 1.93 GHz and 1.12 ms per launch)
+        self.eng.clock_probe(self.out, wgs=self.WGS, delay_us=0, spin_us=1, stream=self.side.cuda_stream)
+        torch.cuda.synchronize(dev)
 
     def start(self, n_launch, est_ms):
         span_us = n_launch * est_ms * 1e3
@@ -537,9 +542,9 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
 
     # the same seals back to back, untimed, until the clock has settled under this load: a C2 launch takes
     # 1.29-1.46 ms for the first few after other work, ~1.0 ms after ~100 ms
-    est_ms = settle(seal_launch, sync, load_settle_ms) or launch_ms(seal_launch, stream, sync)
     lds_kind = lds_cycles_per_launch(batch) is not None
     probe = ClockProbe(eng, dev) if lds_kind else None
+    est_ms = settle(seal_launch, sync, load_settle_ms) or launch_ms(seal_launch, stream, sync)
 
     # kernel time of the same steps from HIP events on the engine's stream; the clock probe beside them
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
