@@ -112,7 +112,10 @@ __device__ unsigned long long g_lat_stamps[16];
 // time (0.325 ms: no wave of it fits beside an AES-GCM workgroup).
 #ifndef ATLS_CHACHA_DBG
 #define ATLS_CHACHA_DBG 0  // timing builds only (wrong results): 1 = no keystream for data slots, 2 = no MAC of
-                           // full seal slots, 4 = no loads or stores of full blocks (PRE >= 2 kernels)
+                           // full seal slots, 4 = no loads or stores of full blocks (PRE >= 2 kernels); round 6
+                           // (the per-record share priced part by part): 8 = no r-power lane scan
+                           // (R = r^4 on every lane), 16 = no lane-combine products (contrib = acc), 32 = no tag
+                           // finish (p_finish), 64 = no r^2 / r^3 / r^4 products (powers = r)
 #endif
 #ifndef ATLS_CHACHA_SOP
 #define ATLS_CHACHA_SOP 1
@@ -306,11 +309,17 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
       r.l[2] = ((r1 >> 20) | (r2 << 12)) & M26;
       r.l[3] = ((r2 >> 14) | (r3 << 18)) & M26;
       r.l[4] = r3 >> 8;
-      rsq = p_mul(r, r);
-      R = p_mul(rsq, rsq);  // r^4
-      if (!LATE) rcu = p_mul(rsq, r);
+      if (ATLS_CHACHA_DBG & 64) {  // timing build: no power products
+        rsq = r;
+        R = r;
+        if (!LATE) rcu = r;
+      } else {
+        rsq = p_mul(r, r);
+        R = p_mul(rsq, rsq);  // r^4
+        if (!LATE) rcu = p_mul(rsq, r);
+      }
 #pragma unroll
-      for (int d = 1; d < GW; d <<= 1) {  // Hillis-Steele prefix product (G = 256: within each wave)
+      for (int d = 1; d < ((ATLS_CHACHA_DBG & 8) ? 1 : GW); d <<= 1) {  // Hillis-Steele prefix product (G = 256: within each wave)
         // one record per wave (the single call): lanes past jL hold no slot, so a record of one step
         // (jL < 32: up to ~1.9 KiB) stops after the levels lanes 0..jL need (5 for an MTU-sized record)
         if (G == 64 && (uint32_t)d > jL) continue;
@@ -535,9 +544,9 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         }
         pw = p_mul(ru, c == 1 ? r : c == 2 ? rsq : rcu);
       }
-      if (!(jf == 0 && na == 0)) contrib = p_mul(acc, pw);
+      if (!(jf == 0 && na == 0)) contrib = (ATLS_CHACHA_DBG & 16) ? acc : p_mul(acc, pw);
     }
-    if (l == jL % G) p_add(contrib, p_mul(innerL, r));
+    if (l == jL % G) p_add(contrib, (ATLS_CHACHA_DBG & 16) ? innerL : p_mul(innerL, r));
   }
   for (int off = GW / 2; off >= 1; off >>= 1) {
     P130 o = p_zero();
@@ -570,7 +579,11 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     }
   }
   uint32_t tag[4];
-  p_finish(contrib, sk, tag);
+  if (ATLS_CHACHA_DBG & 32) {  // timing build: no tag finish
+    tag[0] = contrib.l[0] ^ sk[0]; tag[1] = contrib.l[1] ^ sk[1]; tag[2] = contrib.l[2] ^ sk[2]; tag[3] = contrib.l[3] ^ sk[3];
+  } else {
+    p_finish(contrib, sk, tag);
+  }
   if (G == 64) LAT_STAMP(6, gl == 0);  // lane combine, reduction, tag
 
   if (!OPEN) {

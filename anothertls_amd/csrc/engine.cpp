@@ -603,8 +603,10 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
       gidx = (const uint32_t*)e->grp_idx.p;
       ghdr = (const uint32_t*)((const uint8_t*)e->grp_aux.p + hdr_at);
     }
+    // bit 3: beside the ChaCha20-Poly1305 kernel (gcm.hip gcm_kernel BESIDE: its seal waves leave room for a ChaCha wave)
     rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
-                         (const uint32_t*)e->t0.p, idx, plan_hdr, (uint32_t*)e->err.p, e->n_slots, e->aes_nr_mask,
+                         (const uint32_t*)e->t0.p, idx, plan_hdr, (uint32_t*)e->err.p, e->n_slots,
+                         e->aes_nr_mask | (side ? 8 : 0),
                          gidx, ghdr, e->cus, s, nullptr, 0);
   }
   if (rc) return rc;

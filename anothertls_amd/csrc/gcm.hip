@@ -1139,16 +1139,19 @@ __device__ unsigned long long g_clk_stamps[4];
 template <bool OPEN, int kWaves, int NR>
 __device__ __forceinline__ void gcm_kernel_body(const GcmArgs& A);
 
-// ATLS_GCM_MINW: minimum waves per SIMD of the 12-wave record kernels (__launch_bounds__): 4 caps them at 128
-// VGPRs, so that in a mixed batch a 128-VGPR ChaCha20-Poly1305 wave (chacha_kernel<*, true>) still fits on each
-// SIMD beside the workgroup's three AES-GCM waves (3 x 128 + 128 = 512). The seal kernel had grown to 129
-// VGPRs (136 allocated: 3 x 136 + 128 > 512), which kept the two kernels of a C5 seal off each other's CUs.
-// AES-192 keeps the 168 cap (at 128 its open kernel spills; no mixed config uses it).
+// BESIDE: the seal kernel of a mixed batch, which runs beside the ChaCha20-Poly1305 side kernel (engine.cpp
+// run_batch): capped at 128 VGPRs (minimum ATLS_GCM_MINW = 4 waves per SIMD), so that a 128-VGPR ChaCha20-Poly1305
+// wave (chacha_kernel<false, true>) still fits on each SIMD beside the workgroup's three AES-GCM waves (3 x 128 +
+// 128 = 512). The seal kernel had grown to 129 VGPRs (136 allocated: 3 x 136 + 128 > 512), which kept the two
+// kernels of a C5 seal off each other's SIMDs. Same-box A/B, 3 rounds, parity first (profiles/r06/ab_minw.log):
+// with the cap on every 12-wave kernel C5 seal 0.276-0.281 -> 0.254-0.260 ms (shard), 2.030-2.049 -> 1.900-1.932
+// ms (whole), but C2 seal 0.981-0.987 -> 1.006-1.007 ms and the opens 1-3 % slower -- so only this instance is
+// capped (C2 and every open keep the 168 cap; the open kernel is at 128 anyway).
 #ifndef ATLS_GCM_MINW
 #define ATLS_GCM_MINW 4
 #endif
-template <bool OPEN, int kWaves, int NR>
-__global__ __launch_bounds__(64 * kWaves, (kWaves == 12 && NR != 12) ? ATLS_GCM_MINW : 1) void gcm_kernel(GcmArgs A) {
+template <bool OPEN, int kWaves, int NR, bool BESIDE = false>
+__global__ __launch_bounds__(64 * kWaves, BESIDE ? ATLS_GCM_MINW : 1) void gcm_kernel(GcmArgs A) {
 #ifdef ATLS_CLK_STAMPS
   const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   gcm_kernel_body<OPEN, kWaves, NR>(A);
@@ -1508,7 +1511,8 @@ extern "C" int atls_launch_gcm_single(int open, int nr, const void* ks, uint32_t
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
 }
 
-// nr_mask: bit 0/1/2 = key slots with 10/12/14 rounds exist (one launch each). plan/idx: the
+// nr_mask: bit 0/1/2 = key slots with 10/12/14 rounds exist (one launch each); bit 3 = the seal runs beside a
+// ChaCha20-Poly1305 kernel (a mixed batch: the kernel instance capped at 128 VGPRs). plan/idx: the
 // batch plan of atls_launch_plan, or idx = nullptr for a direct batch (one round count only; the
 // kernel validates and reports through err). gidx/ghdr: a direct batch's key groups
 // (atls_launch_group) or nullptr. grid: workgroups per launch (one per CU). done / done_val: a
@@ -1543,8 +1547,12 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
   uint32_t g = (uint32_t)grid < want ? (uint32_t)grid : want;
   const dim3 block(64 * waves);
   const size_t lds = atls::lds_bytes(waves);
-#define ATLS_LAUNCH_NR(W, NR)                                                                  \
-  if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR>), dim3(g), block, lds, s, A);    \
+  // nr_mask bit 3: a mixed batch's seal beside the ChaCha20-Poly1305 kernel (gcm_kernel BESIDE, AES-128 / -256)
+  const bool beside = (nr_mask & 8) && !open && waves == 12;
+#define ATLS_LAUNCH_NR(W, NR)                                                                           \
+  if (open) hipLaunchKernelGGL((atls::gcm_kernel<true, W, NR>), dim3(g), block, lds, s, A);             \
+  else if (W == 12 && NR != 12 && beside)                                                               \
+    hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR, W == 12 && NR != 12>), dim3(g), block, lds, s, A); \
   else hipLaunchKernelGGL((atls::gcm_kernel<false, W, NR>), dim3(g), block, lds, s, A);
 #define ATLS_LAUNCH(W)                                 \
   if (waves == W) {                                    \
