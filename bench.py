@@ -445,6 +445,7 @@ class ClockProbe:
         self.eng, self.dev = eng, dev
         self.side = torch.cuda.Stream(device=dev)
         self.out = torch.zeros(2 * self.WGS, dtype=torch.int64, device=dev)
+        self.p0, self.p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         # one probe launch here, before any timed window: the first launch of a kernel loads its code object
         # (milliseconds with the host blocked and the GPU idle), which inside the window left the GPU idle and
         # its clock falling (profiles/r06/first/: C2's window at 1.93 GHz and 1.12 ms per launch)
@@ -453,13 +454,24 @@ class ClockProbe:
 
     def start(self, n_launch, est_ms):
         span_us = n_launch * est_ms * 1e3
+        self.p0.record(self.side)
         self.eng.clock_probe(self.out, wgs=self.WGS, delay_us=int(0.15 * span_us), spin_us=max(20, int(0.7 * span_us)),
                              stream=self.side.cuda_stream)
+        self.p1.record(self.side)
 
     def mhz(self):
         torch.cuda.synchronize(self.dev)
         o = self.out.cpu().numpy().reshape(self.WGS, 2).astype(np.float64)
         return float(np.median(100.0 * o[:, 0] / np.maximum(o[:, 1], 1)))
+
+    def overlap(self, w0, w1):
+        """Whether the probe ran inside the window [w0, w1] (HIP events on the engine stream): its end no later
+        than the window's end (+2 %). A probe that could not be placed beside the window's launches reads the
+        clock after them, which is not theirs; the line then says so (clock_in_window false)."""
+        torch.cuda.synchronize(self.dev)
+        win = w0.elapsed_time(w1)
+        end = w0.elapsed_time(self.p1)
+        return {"window_ms": round(win, 3), "probe_end_ms": round(end, 3), "in_window": bool(end <= 1.02 * win + 0.05)}
 
 
 def settle(launch, sync, ms):
@@ -562,7 +574,14 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
             eng.join()
             ev1.record(stream)
 
-    wall = dist.timed_steps(timed_step, steps, warmup, sync, dev)
+    def step_sync():
+        # the engine's streams and torch's current stream, not the probe's side stream: the wall clock of the
+        # timed steps never waits for the probe (were it placed late, it would otherwise stretch the window)
+        eng.sync()
+        torch.cuda.current_stream(dev).synchronize()
+
+    wall = dist.timed_steps(timed_step, steps, warmup, step_sync, dev)
+    sync()
     kern_ms = ev0.elapsed_time(ev1) / steps
     payload = batch["payload"]  # sum of AEAD lengths (content + type byte)
     alg_bytes = 2 * payload + 16 * n
@@ -575,6 +594,8 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
         # the LDS roofline is in cycles: the clock of the timed launches themselves
         m["sclk_mhz"] = probe.mhz()
         m["lds"] = lds_roofline(batch, kern_ms, m["sclk_mhz"], cus)
+        if m["lds"]:
+            m["lds"]["clock_in_window"] = probe.overlap(ev0, ev1)
 
     if do_open:
         # ---- the decrypt half (Gcm::decrypt, gcm.rs:142-157, via record.rs:201-240) over the records
@@ -624,7 +645,8 @@ def measure(name, eng, dev, rank, world, steps, warmup, lazy, records=None, key_
             # the open kernels' LDS-array fraction at the clock of the timed opens themselves
             ol = lds_roofline(batch, open_ms, probe.mhz(), cus)
             if ol:
-                m["open"]["lds"] = {"sclk_MHz": ol["sclk_MHz"], "t_min_ms": ol["t_min_ms"], "frac": ol["frac"]}
+                m["open"]["lds"] = {"sclk_MHz": ol["sclk_MHz"], "t_min_ms": ol["t_min_ms"], "frac": ol["frac"],
+                                    "clock_in_window": probe.overlap(o0, o1)["in_window"]}
         del d_orecs, d_pt, d_res
     if keep:
         m.update(d_in=d_in, d_out=d_out, d_tags=d_tags, d_aux=d_aux, d_recs=d_recs)
