@@ -120,6 +120,9 @@ __device__ unsigned long long g_lat_stamps[16];
 #ifndef ATLS_CHACHA_SOP
 #define ATLS_CHACHA_SOP 1
 #endif
+#ifndef ATLS_CHACHA_KW_RELOAD
+#define ATLS_CHACHA_KW_RELOAD 1  // the planned open kernel reloads the key words per keystream block (chacha_record)
+#endif
 #ifndef ATLS_CHACHA_W2_MAC_FIRST
 #define ATLS_CHACHA_W2_MAC_FIRST 0  // 0: the 2-wave kernel's opens compute the keystream first (it has the registers):
                                     // C3 open 0.0942 -> 0.0896 ms (profiles/r03/ab_c3_open2.log, ab_c3_open.log)
@@ -153,8 +156,13 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   const uint8_t* src = rec_in + ((OPEN && wire) ? 5u : 0u);
   uint8_t* dst = A.out + d.out_off + ((!OPEN && wire) ? 5u : 0u);
 
+  // KW_RELOAD (the planned open: 128-VGPR cap beside AES-GCM, MAC folded before the keystream): the 8 key
+  // words are loaded again (L1 / L2-resident, 32 B) for each keystream block instead of staying live
+  // through the slot's Poly1305 products
+  constexpr bool KW_RELOAD = ATLS_CHACHA_KW_RELOAD && OPEN && G == 16 && LATE && PRE == 0 && !CARRY;
   uint32_t kw[8];
-  for (int i = 0; i < 8; i++) kw[i] = k->kw[i];
+  if (!KW_RELOAD)
+    for (int i = 0; i < 8; i++) kw[i] = k->kw[i];
   uint32_t nw[3];
   uint32_t aad_len = 5, hdr0 = 0, hdr1 = 0;
   const uint8_t* aadp = nullptr;
@@ -178,6 +186,17 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     aad_len = d.aad_len;
     aadp = iv + 12;
   }
+  auto keystream = [&](uint32_t jj, uint32_t (&o)[16]) {
+    if constexpr (KW_RELOAD) {
+      uint64_t kp = reinterpret_cast<uint64_t>(k->kw);
+      asm volatile("" : "+v"(kp));  // opaque: the loads stay at this point instead of being hoisted out of the loop
+      const uint4 a = ld16(reinterpret_cast<const uint8_t*>(kp)), b = ld16(reinterpret_cast<const uint8_t*>(kp) + 16);
+      const uint32_t kx[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+      chacha_block(kx, jj, nw, o);
+    } else {
+      chacha_block(kw, jj, nw, o);
+    }
+  };
   if (G == 64) LAT_STAMP(1, gl == 0);  // descriptor, key words, nonce / AAD in registers
   const uint32_t na = tls ? 1u : (aad_len + 15u) / 16u;
   const uint32_t nct = (n + 15u) / 16u;         // ciphertext pieces (pad16, poly1305.rs:52-56)
@@ -283,7 +302,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
 #pragma unroll
         for (int q = 0; q < 16; q++) ks[q] = kw[q & 7] ^ j;
       } else {
-        chacha_block(kw, j, nw, ks);
+        keystream(j, ks);
       }
     }
     if (G == 64 && base == 0) LAT_STAMP(3, gl == 0);  // keystream blocks
@@ -436,7 +455,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
           } else {
             fold(P);
           }
-          if (MAC_FIRST) chacha_block(kw, j, nw, ks);
+          if (MAC_FIRST) keystream(j, ks);
 #pragma unroll
           for (int q = 0; q < 16; q++) P[q] = skip_xor ? P[q] : (P[q] ^ ks[q]);
           mask_valid(P, valid);

@@ -41,8 +41,10 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
-                               const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val);
+                               const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val,
+                               uint8_t* tail_ws);
 extern "C" size_t atls_group_hdr_offset(uint32_t n_slots);
+extern "C" size_t atls_gcm_tail_bytes(uint32_t n);
 extern "C" int atls_launch_single_resident(uint8_t* blk, uint32_t idle_us, int gcm, hipStream_t s);
 extern "C" int atls_launch_clock_probe(uint32_t wgs, uint32_t delay_us, uint32_t spin_us, uint64_t* out, hipStream_t s);
 extern "C" int atls_launch_sync_flag(const uint32_t* err, uint32_t* out, uint32_t val, hipStream_t s);
@@ -115,6 +117,8 @@ struct atls_engine {
   } ps[2];
   int par = 0, last_par = 0;  // set of the next / the last planned batch
   DevBuf grp_cnt, grp_aux, grp_idx;          // key groups of direct AES-GCM batches (plan.hip)
+  DevBuf tail;                               // deferred last steps of AES-GCM batch records (gcm.hip ATLS_GCM_TAIL)
+  bool tail_on = true;                       // ATLS_GCM_TAIL_ON=0: every record runs its own last step
   uint32_t group_min = 2048;                 // ATLS_GCM_GROUP_MIN: smallest batch to group (0: never)
   int chacha_wgs = 8;                        // ATLS_CHACHA_WGS: ChaCha20-Poly1305 workgroups per CU
   // ATLS_CHACHA_W2: direct ChaCha20-Poly1305 batches take the 2-wave kernel always (2, the default), only when
@@ -268,6 +272,18 @@ void extents(const atls_rec* recs, uint32_t n, bool open, size_t* in_end, size_t
   *aux_end = c;
 }
 
+// The tail workspace of an AES-GCM batch of n records (gcm.hip ATLS_GCM_TAIL), its counters zero; nullptr (no record
+// deferred) when the build or ATLS_GCM_TAIL_ON=0 turns deferral off or the buffer cannot grow.
+uint8_t* tail_ws(atls_engine* e, uint32_t n, hipStream_t s) {
+  const size_t need = atls_gcm_tail_bytes(n);
+  if (!need || !e->tail_on) return nullptr;
+  const size_t cap = e->tail.cap;
+  if (!e->tail.reserve(need)) return nullptr;
+  // the tail kernel zeroes the counters after each batch: a new buffer once
+  if (e->tail.cap != cap && hipMemsetAsync(e->tail.p, 0, 16, s) != hipSuccess) return nullptr;
+  return (uint8_t*)e->tail.p;
+}
+
 // The CU count atls_launch_chacha sizes its 2-wave choice by: 0 never takes it, a huge count always does.
 int w2_cus(const atls_engine* e) { return e->chacha_w2 == 0 ? 0 : e->chacha_w2 == 2 ? (1 << 26) : e->cus; }
 
@@ -281,7 +297,8 @@ int launch_records(atls_engine* e, bool open, const atls_rec* d_recs, uint32_t n
                               w2_cus(e));
   return atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, nullptr, nullptr, (uint32_t*)e->err.p, e->n_slots,
-                         e->aes_nr_mask, nullptr, nullptr, e->cus, s, done, done_val);
+                         e->aes_nr_mask, nullptr, nullptr, e->cus, s, done, done_val,
+                         done ? nullptr : tail_ws(e, n, s));
 }
 
 // Host-memory batch in record-aligned chunks over three streams: every chunk's input goes up on the
@@ -607,7 +624,7 @@ int run_batch(atls_engine* e, bool open, const atls_rec* recs, uint32_t n, const
     rc = atls_launch_gcm(open, e->ks.p, d_recs, n, d_in, d_aux, d_out, d_tags_out, d_tags_in, d_res,
                          (const uint32_t*)e->t0.p, idx, plan_hdr, (uint32_t*)e->err.p, e->n_slots,
                          e->aes_nr_mask | (side ? 8 : 0),
-                         gidx, ghdr, e->cus, s, nullptr, 0);
+                         gidx, ghdr, e->cus, s, nullptr, 0, tail_ws(e, n, s));
   }
   if (rc) return rc;
   if (side) {  // join now, or (lazy) when the set is reused / atls_engine_join / a batch without the flag
@@ -1276,6 +1293,7 @@ atls_engine* atls_engine_create(int device) {
   if (const char* v = std::getenv("ATLS_CHACHA_W2")) e->chacha_w2 = std::atoi(v);
   if (const char* v = std::getenv("ATLS_ZERO_COPY")) e->zero_copy = std::atoi(v);
   if (const char* v = std::getenv("ATLS_GCM_GROUP_MIN")) e->group_min = (uint32_t)std::max(0, std::atoi(v));
+  if (const char* v = std::getenv("ATLS_GCM_TAIL_ON")) e->tail_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("ATLS_SYNC_FLAG")) e->sync_flag = std::atoi(v) != 0;
   if (!e->t0.reserve(256 * 4) || !e->err.reserve(16) || hipMemsetAsync(e->err.p, 0, 16, e->stream) != hipSuccess ||
       atls_launch_build_t0((uint32_t*)e->t0.p, e->stream) ||
@@ -1293,7 +1311,7 @@ void atls_engine_destroy(atls_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->stream2) (void)hipStreamSynchronize(e->stream2);
   for (DevBuf* b : {&e->ks, &e->t0, &e->err, &e->keys_stage, &e->recs, &e->in, &e->out, &e->aux, &e->tags, &e->res,
-                    &e->secrets, &e->dkeys, &e->grp_cnt, &e->grp_aux, &e->grp_idx})
+                    &e->secrets, &e->dkeys, &e->grp_cnt, &e->grp_aux, &e->grp_idx, &e->tail})
     b->release();
   for (auto& q : e->ps) {
     for (DevBuf* b : {&q.plan, &q.keys, &q.idx, &q.wg}) b->release();

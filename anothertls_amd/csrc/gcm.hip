@@ -334,6 +334,36 @@ __device__ unsigned long long g_tt_stamps[16];
 #define ATLS_GEN_PN 0
 #endif
 
+// Deferred last steps (round 6). A one-record-per-wave record of S slots runs ceil(S / 64) wave
+// steps; its last step holds rem = S - 64 floor((S - 1) / 64) slots, yet costs a whole step's LDS lookups and VALU
+// issue (a C2 record: 1,028 slots, the 17th step 4 lanes of 64 -- 5.5 % of C2 with a key per record,
+// profiles/r05/ab_keyrec_parts.log; the LDS array serves a lane group whether 4 or 32 of its lanes are enabled).
+// With ATLS_GCM_TAIL = T > 0, a batch launch's record whose last step has rem <= T slots stops after its full
+// steps: the lane combine runs for the first S - rem slots (Z' = the GHASH state after them), and lane 0 leaves
+// Z', E_K(J0) and (opens) the content-type scan in the launch's tail workspace. gcm_tail_kernel then finishes
+// those records one per lane: the rem slots' counter blocks by T-table AES with the lane's own round keys,
+// their ciphertext, Z' <- (Z' ^ B) * H over the rem GHASH blocks (comb multiply, per-lane H), the tag or the
+// open's verdict. Records that go through lane groups, the single call, WIRE records and non-96-bit IVs keep
+// their last step.
+// Measured and left off (profiles/r06/tail/: parity green, 60 tests; same box, 3 interleaved rounds, engine switch
+// ATLS_GCM_TAIL_ON): C2 with a key per record 1.293-1.299 ms deferred vs 1.252-1.259 not, C2 1.050-1.060 vs
+// 1.025-1.037, C4 shard 2.621-2.635 vs 2.569-2.612, C5 whole within noise. rocprof (keyrec): the record kernel
+// 1.2218 vs 1.2486 ms (-27 us, 2.2 %: the kernel is not bound by the steps it no longer runs) and the tail kernel
+// 74 us for 65,536 records (key-schedule gathers from HBM, one AES block and one comb product per lane). Even a free
+// tail kernel would buy 2 %; 0 compiles every piece of it out.
+#ifndef ATLS_GCM_TAIL
+#define ATLS_GCM_TAIL 0
+#endif
+struct TailState {  // one deferred record (48 B): Z' (be words), E_K(J0) (raw words), open scan, record index
+  uint32_t z[4];
+  uint32_t e[4];
+  int64_t lastnz;
+  uint32_t rec;
+  uint32_t pad;
+};
+// Tail workspace: [0] deferred count, [1] tail workgroups done, [2..3] pad, then TailState[n] from byte 16.
+constexpr size_t kTailHdr = 16;
+
 // LAT: the single-call kernel's record (one wave's latency, no occupancy to keep): the branch-free first
 // step (ATLS_SINGLE_FAST_FIRST) and the LDS lane combine at every key size.
 // LN: the threads that share the record -- 64 (one wave: the batch kernels), or 256 (the single-call
@@ -421,6 +451,12 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   const uint32_t m = na + nb + 1u;  // GHASH blocks: AAD, data, length
   const uint32_t S = m + 1u;        // slots: E(J0) + GHASH blocks
   const uint32_t in_bytes = len;    // bytes readable from src
+  // ATLS_GCM_TAIL: a sparse last step is left to gcm_tail_kernel; the steps and the lane combine run over the
+  // first S_run slots (S_run = S otherwise)
+  const uint32_t rem = S - (uint32_t)LN * ((S - 1u) / (uint32_t)LN);
+  const bool defer = ATLS_GCM_TAIL > 0 && LN == 64 && !LAT && A.tail != nullptr && is96 && na == 1u && !wire &&
+                     S > (uint32_t)LN && S <= 64u * 256u && rem <= (uint32_t)ATLS_GCM_TAIL;
+  const uint32_t S_run = defer ? S - rem : S, m_run = S_run - 1u;
 
   // A record of one step (S <= 64: AEAD up to 976 B in TLS mode) multiplies nothing by H^64:
   // Y starts at 0 and the lane combine applies every power, so it skips the table.
@@ -483,9 +519,9 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   // Lane combine exponent (see below): s_last = the lane's last slot holding a GHASH block (slots
   // 1..m), -1 if none.
   int64_t s_last = -1;
-  if (lane == 0) { if (m >= (uint32_t)LN) s_last = (int64_t)(m / LN) * LN; }
-  else if ((uint32_t)lane <= m) s_last = (int64_t)lane + (int64_t)((m - (uint32_t)lane) / LN) * LN;
-  const uint32_t e_comb = s_last >= 1 ? S - (uint32_t)s_last : 1u;  // 1..LN
+  if (lane == 0) { if (m_run >= (uint32_t)LN) s_last = (int64_t)(m_run / LN) * LN; }
+  else if ((uint32_t)lane <= m_run) s_last = (int64_t)lane + (int64_t)((m_run - (uint32_t)lane) / LN) * LN;
+  const uint32_t e_comb = s_last >= 1 ? S_run - (uint32_t)s_last : 1u;  // 1..LN
   // the lane's combine multiplier H^e_comb, loaded now so its latency hides under the steps
   uint32_t hp[4];
 #pragma unroll
@@ -508,7 +544,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
   const uint32_t lim = min(in_bytes, n_aead);
   const bool first_fast = (LAT ? ATLS_SINGLE_FAST_FIRST : ATLS_GCM_FAST_FIRST) && use_cache && !(OPEN && wire) && fast_end >= (uint32_t)LN;  // TLS / WIRE / RAW (one AAD block)
   TT_STAMP(t_setup);
-  for (uint32_t base = 0; base < S; base += LN) {
+  for (uint32_t base = 0; base < S_run; base += LN) {
     TT_STAMP(t_step);
     const uint32_t s = base + (uint32_t)lane;
     if (base >= (uint32_t)LN && base + LN <= fast_end) {  // wave-uniform
@@ -760,6 +796,25 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
         }
       }
     }
+  }
+  if (defer) {  // the record's last slots, tag and verdict: gcm_tail_kernel
+    if (OPEN && tls) {
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) {
+        const int64_t o = __shfl_xor(lastnz, off, 64);
+        lastnz = o > lastnz ? o : lastnz;
+      }
+    }
+    if (lane == 0) {
+      uint32_t* hdr = reinterpret_cast<uint32_t*>(A.tail);
+      const uint32_t slot = atomicAdd(hdr, 1u);
+      TailState* ts = reinterpret_cast<TailState*>(A.tail + kTailHdr) + slot;
+      st16(reinterpret_cast<uint8_t*>(ts->z), make_uint4(z[0], z[1], z[2], z[3]));
+      st16(reinterpret_cast<uint8_t*>(ts->e), make_uint4(e0, e1, e2, e3));
+      ts->lastnz = lastnz;
+      ts->rec = rec_idx;
+    }
+    return;
   }
   const uint32_t t0 = e0 ^ bswap32(z[0]), t1 = e1 ^ bswap32(z[1]), t2 = e2 ^ bswap32(z[2]), t3 = e3 ^ bswap32(z[3]);
 
@@ -1265,6 +1320,157 @@ __device__ __forceinline__ void gcm_kernel_body(const GcmArgs& A) {
   }
 }
 
+// ---- deferred last steps (ATLS_GCM_TAIL) ----------------------------------------------------
+// A deferred record's last rem slots (data blocks and the length block; S_run >= 64 puts the AAD in the full
+// steps) on kTailLanes lanes: lane gl takes tail slots i = gl, gl + kTailLanes, ... -- the counter block by T-table
+// AES with the lane's own round keys (vector loads from its key schedule) against the workgroup's replicated
+// T-tables, the ciphertext, and the slot's GHASH term. From Z' = X_{S_run - 1}, the Horner steps X <- (X ^ B_i) * H
+// over the rem blocks (gcm.rs:88-121) unroll to X = (Z' ^ B_0) * H^rem ^ sum_{i >= 1} B_i * H^(rem - i), so each
+// term is one independent product by a power from the key schedule (hpow_be, gf_mul_comb: the reference's gmult
+// product, gcm.rs:21-40) and the group XORs its terms -- one AES block and one product deep per lane.
+constexpr int kTailLanes = 4;
+template <int NR, bool OPEN>
+__device__ __forceinline__ void tail_record(const GcmArgs& A, const TailState& ts, uint32_t lb, uint32_t gl) {
+  const uint32_t r = ts.rec;
+  const atls_rec d = A.recs[r];
+  const KeySched* k = A.ks + d.key_slot;
+  const bool tls = d.mode != ATLS_MODE_RAW;  // (WIRE records are never deferred)
+  const uint32_t len = d.len;
+  const uint32_t n_aead = (tls && !OPEN) ? len + 1 : len;
+  const uint32_t na = 1u, nb = (n_aead + 15u) / 16u, m = na + nb + 1u, S = m + 1u;
+  const uint32_t rem = S - 64u * ((S - 1u) / 64u), S_run = S - rem;
+  uint32_t x[4] = {0, 0, 0, 0};
+  int64_t lastnz = -1;
+  if (gl < rem) {
+    uint32_t rk[4 * (NR + 1)], rkr[4 * (NR + 1)];
+#pragma unroll
+    for (int i = 0; i < NR + 1; i++) {
+      const uint4 a = ld16(reinterpret_cast<const uint8_t*>(k->rk + 4 * i));
+      const uint4 b = ld16(reinterpret_cast<const uint8_t*>(k->rkr + 4 * i));
+      rk[4 * i] = a.x; rk[4 * i + 1] = a.y; rk[4 * i + 2] = a.z; rk[4 * i + 3] = a.w;
+      rkr[4 * i] = b.x; rkr[4 * i + 1] = b.y; rkr[4 * i + 2] = b.z; rkr[4 * i + 3] = b.w;
+    }
+    const uint8_t* src = A.in + d.in_off;
+    uint8_t* dst = A.out + d.out_off;
+    uint32_t j0[3];  // be words of the 96-bit nonce; J0 = nonce || 1 (gcm.rs:59-74)
+    if (tls) {
+      const uint64_t seq = d.seq;
+      j0[0] = bswap32(k->siv[0]);
+      j0[1] = bswap32(k->siv[1]) ^ (uint32_t)(seq >> 32);
+      j0[2] = bswap32(k->siv[2]) ^ (uint32_t)seq;
+    } else {
+      const uint8_t* iv = A.aux + d.aux_off;
+#pragma unroll
+      for (int w = 0; w < 3; w++)
+        j0[w] = ((uint32_t)iv[4 * w] << 24) | ((uint32_t)iv[4 * w + 1] << 16) | ((uint32_t)iv[4 * w + 2] << 8) | iv[4 * w + 3];
+    }
+    const uint32_t aad_len = tls ? 5u : d.aad_len;
+    for (uint32_t i = gl; i < rem; i += (uint32_t)kTailLanes) {
+      const uint32_t sl = S_run + i, g = sl - 1u;  // slot sl holds GHASH block g
+      uint32_t B[4] = {0, 0, 0, 0};
+      if (g < na + nb) {  // data block, counter J0 + sl - na (gcm.rs:89-96)
+        const uint32_t off = (g - na) * 16u, valid = min(16u, n_aead - off);
+        uint32_t st[4] = {bswap32(j0[0]), bswap32(j0[1]), bswap32(j0[2]), bswap32(1u + (sl - na))};
+        aes_encrypt_tt<NR>(st, rk, rkr, lb);
+        uint32_t P[4] = {0, 0, 0, 0};
+        if (valid == 16u && off + 16u <= len) {
+          const uint4 v = ld16(src + off);
+          P[0] = v.x; P[1] = v.y; P[2] = v.z; P[3] = v.w;
+        } else {
+          for (uint32_t q = 0; q < valid; q++)  // past the input only the TLS content type (record.rs:173)
+            P[q >> 2] |= ((off + q < len) ? (uint32_t)src[off + q] : (uint32_t)d.content_type) << (8 * (q & 3));
+        }
+        uint32_t C[4] = {P[0] ^ st[0], P[1] ^ st[1], P[2] ^ st[2], P[3] ^ st[3]};
+#pragma unroll
+        for (int w = 0; w < 4; w++) {  // only `valid` bytes exist
+          const int lo = 4 * w;
+          if ((int)valid < lo + 4) C[w] &= ((int)valid <= lo) ? 0u : (0xffffffffu >> (8 * (lo + 4 - (int)valid)));
+        }
+        if (valid == 16u) {
+          st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
+        } else {
+          for (uint32_t q = 0; q < valid; q++) dst[off + q] = (uint8_t)(C[q >> 2] >> (8 * (q & 3)));
+        }
+        if (OPEN && tls) {
+          const int jn = last_nonzero(C, (int)valid);
+          if (jn >= 0) lastnz = ((int64_t)(off + (uint32_t)jn) << 8) | ((C[jn >> 2] >> (8 * (jn & 3))) & 0xffu);
+        }
+#pragma unroll
+        for (int w = 0; w < 4; w++) B[w] = OPEN ? P[w] : C[w];
+      } else {  // length block: [len(A)]_64 || [len(C)]_64 in bits (gcm.rs:121)
+        const uint64_t abits = (uint64_t)aad_len * 8u, cbits = (uint64_t)n_aead * 8u;
+        B[0] = bswap32((uint32_t)(abits >> 32)); B[1] = bswap32((uint32_t)abits);
+        B[2] = bswap32((uint32_t)(cbits >> 32)); B[3] = bswap32((uint32_t)cbits);
+      }
+      uint32_t v[4] = {bswap32(B[0]), bswap32(B[1]), bswap32(B[2]), bswap32(B[3])}, hp[4], pr[4];
+      if (i == 0) {
+#pragma unroll
+        for (int w = 0; w < 4; w++) v[w] ^= ts.z[w];
+      }
+#pragma unroll
+      for (int w = 0; w < 4; w++) hp[w] = k->hpow_be[rem - i - 1u][w];  // H^(rem - i)
+      gf_mul_comb(v, hp, pr);
+#pragma unroll
+      for (int w = 0; w < 4; w++) x[w] ^= pr[w];
+    }
+  }
+  // the group's terms and (opens) content-type scans; lanes of a group are adjacent, the group is whole
+#pragma unroll
+  for (int off = kTailLanes / 2; off >= 1; off >>= 1) {
+#pragma unroll
+    for (int w = 0; w < 4; w++) x[w] ^= (uint32_t)__shfl_xor((int)x[w], off, kTailLanes);
+    if (OPEN) {
+      const int64_t o = __shfl_xor(lastnz, off, kTailLanes);
+      lastnz = o > lastnz ? o : lastnz;
+    }
+  }
+  if (gl != 0) return;
+  if (OPEN && ts.lastnz > lastnz) lastnz = ts.lastnz;  // nothing non-zero in the tail: the full steps' scan
+  const uint32_t t0 = ts.e[0] ^ bswap32(x[0]), t1 = ts.e[1] ^ bswap32(x[1]), t2 = ts.e[2] ^ bswap32(x[2]),
+                 t3 = ts.e[3] ^ bswap32(x[3]);
+  if (!OPEN) {
+    if (A.tags_out) st16(A.tags_out + 16ull * r, make_uint4(t0, t1, t2, t3));
+  } else {
+    const uint4 tg = ld16(A.tags_in + 16ull * r);
+    const bool ok = (tg.x == t0) & (tg.y == t1) & (tg.z == t2) & (tg.w == t3);
+    write_open_result(A, r, tls, len, ok, lastnz, true);
+  }
+}
+
+// The deferred records of the launch(es) just before it on the stream, kTailLanes threads per record; the last
+// workgroup to finish zeroes the workspace's counters for the next batch (no memset launch).
+constexpr int kTailThreads = 256;
+template <bool OPEN>
+__global__ __launch_bounds__(kTailThreads) void gcm_tail_kernel(GcmArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* hdr = reinterpret_cast<uint32_t*>(A.tail);
+  const uint32_t cnt = __hip_atomic_load(hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  constexpr uint32_t kPer = kTailThreads / kTailLanes;  // records per workgroup pass
+  if (blockIdx.x * kPer < cnt) {
+    build_ttables<kTailThreads>(smem, A.t0, (int)threadIdx.x);
+    const uint32_t lb = 4u * (threadIdx.x & 31u), gl = threadIdx.x % (uint32_t)kTailLanes;
+    const TailState* st = reinterpret_cast<const TailState*>(A.tail + kTailHdr);
+    for (uint32_t i0 = blockIdx.x * kPer; i0 < cnt; i0 += gridDim.x * kPer) {  // workgroup-uniform trip count
+      const uint32_t i = i0 + threadIdx.x / (uint32_t)kTailLanes;
+      if (i < cnt) {
+        const TailState ts = st[i];
+        const uint32_t nr = A.ks[A.recs[ts.rec].key_slot].nr;
+        if (nr == 10) tail_record<10, OPEN>(A, ts, lb, gl);
+        else if (nr == 12) tail_record<12, OPEN>(A, ts, lb, gl);
+        else tail_record<14, OPEN>(A, ts, lb, gl);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(hdr + 1, 1u) == gridDim.x - 1u) {  // every workgroup has read the count
+      __hip_atomic_store(hdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(hdr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // The single call with its descriptor, IV || AAD, input and received tag in the launch's argument block
 // (kSingleInline bytes at most; chacha.hip chacha_single has the same layout): 4 waves build the T-tables,
 // wave 0 seals / opens the record and sets the completion flag. The record's key schedule (device memory)
@@ -1521,11 +1727,13 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
                                const uint8_t* aux, uint8_t* out, uint8_t* tags_out, const uint8_t* tags_in,
                                atls_open_result* res, const uint32_t* t0, const uint32_t* idx, void* plan,
                                uint32_t* err, uint32_t n_slots, int nr_mask, const uint32_t* gidx,
-                               const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val) {
+                               const uint32_t* ghdr, int grid, hipStream_t s, uint32_t* done, uint32_t done_val,
+                               uint8_t* tail_ws) {
   if (n == 0) return 0;
   atls::GcmArgs A{(const atls::KeySched*)ks, recs, n, in, aux, out, tags_out, tags_in, res, t0, idx,
                   (atls::PlanHdr*)plan, err, n_slots, idx ? nullptr : gidx,
-                  (atls::GroupHdr*)const_cast<uint32_t*>(ghdr), n == 1 ? done : nullptr, done_val};
+                  (atls::GroupHdr*)const_cast<uint32_t*>(ghdr), n == 1 ? done : nullptr, done_val,
+                  (n == 1 && done) ? nullptr : tail_ws};
   if (n == 1 && done && !idx && !gidx && __builtin_popcount((unsigned)nr_mask) == 1) {  // the single call's longer records: 4 waves
     const dim3 b1(64 * atls::kSingleWaves);
 #define ATLS_SINGLE_PTR(NR)                                                                            \
@@ -1566,7 +1774,19 @@ extern "C" int atls_launch_gcm(int open, const void* ks, const atls_rec* recs, u
 #endif
 #undef ATLS_LAUNCH
 #undef ATLS_LAUNCH_NR
+  if (A.tail && ATLS_GCM_TAIL > 0) {  // the deferred last steps of the launch(es) above (ATLS_GCM_TAIL)
+    constexpr uint32_t per = atls::kTailThreads / atls::kTailLanes;
+    const uint32_t want_t = (n + per - 1u) / per, cap_t = 4u * (uint32_t)grid;
+    const size_t lds_t = atls::kTabBytes + 1024;  // the T-tables and build_ttables' staging row
+    if (open) hipLaunchKernelGGL(atls::gcm_tail_kernel<true>, dim3(want_t < cap_t ? want_t : cap_t), dim3(atls::kTailThreads), lds_t, s, A);
+    else hipLaunchKernelGGL(atls::gcm_tail_kernel<false>, dim3(want_t < cap_t ? want_t : cap_t), dim3(atls::kTailThreads), lds_t, s, A);
+  }
   return hipGetLastError() == hipSuccess ? 0 : ATLS_INTERNAL_ERROR;
+}
+
+// Bytes of the tail workspace a batch of n records needs (engine.cpp; 0 when the build defers nothing).
+extern "C" size_t atls_gcm_tail_bytes(uint32_t n) {
+  return ATLS_GCM_TAIL > 0 ? atls::kTailHdr + sizeof(atls::TailState) * (size_t)n : 0;
 }
 
 // Compile-time experiment switches this library was built with (include/atls.h

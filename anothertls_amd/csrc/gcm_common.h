@@ -356,6 +356,7 @@ struct GcmArgs {
   GroupHdr* ghdr;          // their region sizes and work counters
   uint32_t* done;          // one-record direct launch (the single call): set to done_val when the
   uint32_t done_val;       // record's outputs are visible system-wide (mapped host memory), or nullptr
+  uint8_t* tail;           // batch launches: workspace of the deferred last steps (gcm.hip gcm_tail_kernel), or nullptr
 };
 
 // The single call's completion flag: after the wave's own stores have left (system-scope release),

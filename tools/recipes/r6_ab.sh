@@ -8,14 +8,14 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 tag=$1
-mkdir -p gpurun_out/r6
-out=gpurun_out/r6/ab_$tag.log
+mkdir -p ${O:-gpurun_out/r6}
+out=${O:-gpurun_out/r6}/ab_$tag.log
 : > $out
 if [ "${PARITY:-1}" = 1 ]; then
   for v in ${VARIANTS:-base}; do
     lib=anothertls_amd/variants/libatls_$v.so
-    ATLS_LIB=$PWD/$lib timeout -k 10 500 python -u -m pytest ${PARITY_TESTS:-tests/test_gpu_parity.py tests/test_gpu_plan.py tests/test_wire_mode.py tests/test_gpu_gcm_groups.py tests/test_gpu_configs.py} -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/r6/ab_${tag}_parity_$v.txt 2>&1 || { echo "$v parity FAILED" >> $out; tail -30 gpurun_out/r6/ab_${tag}_parity_$v.txt; exit 1; }
-    echo "$v parity: $(tail -1 gpurun_out/r6/ab_${tag}_parity_$v.txt)" >> $out
+    ATLS_LIB=$PWD/$lib timeout -k 10 500 python -u -m pytest ${PARITY_TESTS:-tests/test_gpu_parity.py tests/test_gpu_plan.py tests/test_wire_mode.py tests/test_gpu_gcm_groups.py tests/test_gpu_configs.py} -x -q -m gpu --timeout 300 --timeout-method thread > ${O:-gpurun_out/r6}/ab_${tag}_parity_$v.txt 2>&1 || { echo "$v parity FAILED" >> $out; tail -30 ${O:-gpurun_out/r6}/ab_${tag}_parity_$v.txt; exit 1; }
+    echo "$v parity: $(tail -1 ${O:-gpurun_out/r6}/ab_${tag}_parity_$v.txt)" >> $out
   done
 fi
 for round in $(seq 1 ${ROUNDS:-3}); do
