@@ -115,7 +115,8 @@ __device__ unsigned long long g_lat_stamps[16];
                            // full seal slots, 4 = no loads or stores of full blocks (PRE >= 2 kernels); round 6
                            // (the per-record share priced part by part): 8 = no r-power lane scan
                            // (R = r^4 on every lane), 16 = no lane-combine products (contrib = acc), 32 = no tag
-                           // finish (p_finish), 64 = no r^2 / r^3 / r^4 products (powers = r)
+                           // finish (p_finish), 64 = no r^2 / r^3 / r^4 products (powers = r), 128 = direct
+                           // batches: a wave reads its step's record lengths and does nothing else (the launch floor)
 #endif
 #ifndef ATLS_CHACHA_SOP
 #define ATLS_CHACHA_SOP 1
@@ -212,7 +213,9 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   P130 r256 = p_zero(), r512 = p_zero(), r768 = p_zero();  // G = 256: wave factors
   uint32_t sk[4] = {0, 0, 0, 0};
   P130 acc = p_zero(), innerL = p_zero();
-  int64_t lastnz = -1;
+  // open: ((offset + 1) << 8) | byte of the last non-zero plaintext byte, 0 = none (32 bits: ChaCha20-Poly1305
+  // records are < 2^24 bytes, plan.h chacha_len_ok; one VGPR instead of a 64-bit pair)
+  uint32_t lastnz = 0;
   constexpr bool MAC_FIRST = OPEN && G != 64 && (PRE < 2 || ATLS_CHACHA_W2_MAC_FIRST) &&
                              (CARRY ? ATLS_CHACHA_OPEN_MAC_FIRST >= 2 : ATLS_CHACHA_OPEN_MAC_FIRST >= 1);
   constexpr bool SOP = ATLS_CHACHA_SOP && !LATE;  // full slots: one reduction (p_sop4)
@@ -373,7 +376,9 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     uint32_t cnt = 0;
     bool sop = false;
     if (j == 0) {  // AAD blocks (get_mac_data: aad || pad16, poly1305.rs:57-59)
-      for (uint32_t i = 0; i < na; i++) {
+      uint32_t al = aad_len;  // na blocks; the bound is derived here, behind an opaque copy, so that no trip count is
+      asm volatile("" : "+v"(al));  // hoisted and kept live through the slot loop (the planned open spilled it)
+      for (uint32_t i = 0; 16u * i < al; i++) {
         uint32_t B[4] = {0, 0, 0, 0};
         if (tls) {
           B[0] = hdr0; B[1] = hdr1;
@@ -500,7 +505,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
             for (int q = 15; q >= 0; q--) {
               if (P[q]) {
                 const int bi = 4 * q + (31 - __builtin_clz(P[q])) / 8;
-                lastnz = ((int64_t)(off + bi) << 8) | ((P[q] >> (8 * (bi & 3))) & 0xffu);
+                lastnz = ((off + (uint32_t)bi + 1u) << 8) | ((P[q] >> (8 * (bi & 3))) & 0xffu);
                 break;
               }
             }
@@ -575,12 +580,11 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   if constexpr (G > 64) {  // the waves' partial sums (and content-type maxima) meet in LDS
     if (OPEN) {
       for (int off = 32; off >= 1; off >>= 1) {
-        const int64_t o = __shfl_xor(lastnz, off, 64);
-        lastnz = o > lastnz ? o : lastnz;
+        lastnz = max(lastnz, (uint32_t)__shfl_xor((int)lastnz, off, 64));
       }
     }
     __shared__ uint32_t xc[G / 64][5];
-    __shared__ int64_t xl[G / 64];
+    __shared__ uint32_t xl[G / 64];
     p_carry(contrib);  // limbs < 2^26 again, so four partials add without overflow
     if ((gl & 63) == 0) {
 #pragma unroll
@@ -619,8 +623,7 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
   } else {
     if (G <= 64) {
       for (int off = G / 2; off >= 1; off >>= 1) {
-        const int64_t o = __shfl_xor(lastnz, off, G);
-        lastnz = o > lastnz ? o : lastnz;
+        lastnz = max(lastnz, (uint32_t)__shfl_xor((int)lastnz, off, G));
       }
     }
     if (gl == 0) {
@@ -641,10 +644,10 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
         rr.content_len = 0;
         rr.content_type = 0;
       } else {
-        const uint32_t ty = lastnz >= 0 ? (uint32_t)(lastnz & 0xff) : 0u;
+        const uint32_t ty = lastnz & 0xffu;
         const bool vt = ty == 0 || ty == 20 || ty == 21 || ty == 22 || ty == 23;
         rr.status = vt ? ATLS_OK : ATLS_DECODE_ERROR;
-        rr.content_len = (vt && lastnz >= 0) ? (uint32_t)(lastnz >> 8) : 0u;
+        rr.content_len = (vt && lastnz) ? (lastnz >> 8) - 1u : 0u;
         rr.content_type = vt ? (uint8_t)ty : 0;
       }
       A.res[rec_idx] = rr;
@@ -796,6 +799,10 @@ __device__ __forceinline__ void chacha_direct(const ChArgs& A, int lane) {
 #pragma unroll
     for (int off = (int)P / 2; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
     mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
+    if (ATLS_CHACHA_DBG & 128) {  // timing build: the launch floor (no record is processed)
+      if (mx == 0xffffffffu) A.err[0] = 1u;  // keeps the length reads
+      continue;
+    }
     if (ATLS_CHACHA_STAGE && !OPEN && PRE >= 2 && ATLS_CHACHA_TINY && mx <= (uint32_t)ATLS_CHACHA_TINY &&
         q0 + P <= cnt) {
       // STAGE needs every lane in the same steps: a full wave step of TLS / RAW records of one length,
