@@ -116,7 +116,8 @@ __device__ unsigned long long g_lat_stamps[16];
                            // (the per-record share priced part by part): 8 = no r-power lane scan
                            // (R = r^4 on every lane), 16 = no lane-combine products (contrib = acc), 32 = no tag
                            // finish (p_finish), 64 = no r^2 / r^3 / r^4 products (powers = r), 128 = direct
-                           // batches: a wave reads its step's record lengths and does nothing else (the launch floor)
+                           // batches: a wave reads its step's record lengths and does nothing else (the launch floor),
+                           // 256 (with 1) = no key-block keystream either
 #endif
 #ifndef ATLS_CHACHA_SOP
 #define ATLS_CHACHA_SOP 1
@@ -301,7 +302,8 @@ __device__ void chacha_record(const ChArgs& A, const atls_rec& d, const KeySched
     if (G == 64 && base == 0) LAT_STAMP(2, gl == 0);  // the step's data blocks loaded
     uint32_t ks[16];
     if (active && j <= jmax && (!MAC_FIRST || j == 0)) {
-      if ((ATLS_CHACHA_DBG & 1) && j) {  // timing build: no keystream for data slots (wrong output)
+      if ((ATLS_CHACHA_DBG & 1) != 0 && (j != 0u || (ATLS_CHACHA_DBG & 256) != 0)) {  // timing build: no keystream for data slots
+        // (wrong output); with 256 none for the Poly1305 key block either
 #pragma unroll
         for (int q = 0; q < 16; q++) ks[q] = kw[q & 7] ^ j;
       } else {
