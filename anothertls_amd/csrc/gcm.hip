@@ -33,9 +33,6 @@
 
 namespace atls {
 
-#ifndef ATLS_GHASH_W
-#define ATLS_GHASH_W 0  // > 0: GHASH lookups issued per LDS round trip (ghash_mul_tab_wide); 0: compiler schedule
-#endif
 #ifndef ATLS_DBG_SKIP
 #define ATLS_DBG_SKIP 0  // timing experiments only (wrong results): 1 lane combine, 2 general steps, 4 GHASH
                          // table, 8 GHASH multiply in general steps, 16 last step, 32 first step,
@@ -104,11 +101,10 @@ __device__ __forceinline__ void lane_comb(const uint32_t (&yb)[4], const uint32_
   else gf_mul_comb(yb, hp, z);
 }
 
-template <int W>
-__device__ __forceinline__ void ghash_mul(uint32_t (&y)[4], uint32_t wb) {
-  if constexpr (W == 0) ghash_mul_tab(y, wb);
-  else ghash_mul_tab_wide<W>(y, wb);
-}
+// The GHASH product of every record kernel: the compiler's schedule of the 32 lookups. The former ATLS_GHASH_W
+// switch (ghash_mul_tab_wide, W lookups per LDS round trip) was removed in round 6: re-tried at W = 16 it gave wrong
+// tags on some records of the mixed parity batch (tests/test_gpu_parity.py), and no round measured it faster.
+__device__ __forceinline__ void ghash_mul(uint32_t (&y)[4], uint32_t wb) { ghash_mul_tab(y, wb); }
 
 // Round-key words from the key schedule: a wave-uniform address, so one s_load_dwordx4.
 __device__ __forceinline__ v4u32 kload4(const uint32_t* p) {
@@ -570,7 +566,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
       st16(dst + off, make_uint4(C.x, C.y, C.z, C.w));
       if (OPEN && tls) lastnz = block_last_nz(C.x, C.y, C.z, C.w, off, lastnz);
       const v4u32 Bv = OPEN ? P : C;
-      ghash_mul<ATLS_GHASH_W>(y, wh);
+      ghash_mul(y, wh);
       y[0] ^= Bv.x; y[1] ^= Bv.y; y[2] ^= Bv.z; y[3] ^= Bv.w;
 #ifdef ATLS_TT_STAMPS
       t_fast += __builtin_amdgcn_s_memtime() - t_step;
@@ -745,7 +741,7 @@ __device__ void gcm_record(const GcmArgs& A, const atls_rec& d, const KeySched* 
     }
     // Y <- Y * H^64 ^ B on the lanes that hold a GHASH block; the others keep Y (s_last below).
     uint32_t yn[4] = {y[0], y[1], y[2], y[3]};
-    if (base && !(ATLS_DBG_SKIP & 8) && live) ghash_mul<ATLS_GHASH_W>(yn, wh);  // Y = 0 before the first step
+    if (base && !(ATLS_DBG_SKIP & 8) && live) ghash_mul(yn, wh);  // Y = 0 before the first step
     if (s >= 1 && s <= m) {
 #pragma unroll
       for (int w = 0; w < 4; w++) y[w] = yn[w] ^ B[w];
@@ -1025,10 +1021,10 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
         st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
         st16(dst + off2, make_uint4(D[0], D[1], D[2], D[3]));
         if (OPEN) lastnz = block_last_nz(D[0], D[1], D[2], D[3], off2, block_last_nz(C[0], C[1], C[2], C[3], off, lastnz));
-        ghash_mul<ATLS_GHASH_W>(y, wb);
+        ghash_mul(y, wb);
         if (OPEN) { y[0] ^= Pu.x; y[1] ^= Pu.y; y[2] ^= Pu.z; y[3] ^= Pu.w; }
         else { y[0] ^= C[0]; y[1] ^= C[1]; y[2] ^= C[2]; y[3] ^= C[3]; }
-        ghash_mul<ATLS_GHASH_W>(y, wb);
+        ghash_mul(y, wb);
         if (OPEN) { y[0] ^= Pv.x; y[1] ^= Pv.y; y[2] ^= Pv.z; y[3] ^= Pv.w; }
         else { y[0] ^= D[0]; y[1] ^= D[1]; y[2] ^= D[2]; y[3] ^= D[3]; }
         t++;
@@ -1047,7 +1043,7 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
       const uint32_t C[4] = {Pu.x ^ st[0], Pu.y ^ st[1], Pu.z ^ st[2], Pu.w ^ st[3]};
       st16(dst + off, make_uint4(C[0], C[1], C[2], C[3]));
       if (OPEN) lastnz = block_last_nz(C[0], C[1], C[2], C[3], off, lastnz);
-      ghash_mul<ATLS_GHASH_W>(y, wb);
+      ghash_mul(y, wb);
       if (OPEN) { y[0] ^= Pu.x; y[1] ^= Pu.y; y[2] ^= Pu.z; y[3] ^= Pu.w; }
       else { y[0] ^= C[0]; y[1] ^= C[1]; y[2] ^= C[2]; y[3] ^= C[3]; }
       continue;
@@ -1114,7 +1110,7 @@ __device__ void gcm_group(const GcmArgs& A, const KeySched* k, uint32_t rec_idx,
       B[2] = bswap32((uint32_t)(cbits >> 32)); B[3] = bswap32((uint32_t)cbits);
     }
     uint32_t yn[4] = {y[0], y[1], y[2], y[3]};
-    if (base) ghash_mul<ATLS_GHASH_W>(yn, wb);
+    if (base) ghash_mul(yn, wb);
     if (s >= 1u && s <= m) {
 #pragma unroll
       for (int w = 0; w < 4; w++) y[w] = yn[w] ^ B[w];
@@ -1796,7 +1792,6 @@ extern "C" unsigned atls_build_flags(void) {
   unsigned f = 0;
   if (ATLS_DBG_SKIP || atls_chacha_dbg()) f |= ATLS_BUILD_DBG_SKIP;
   if (ATLS_DBG_SHARED_GHASH) f |= ATLS_BUILD_DBG_SHARED_GHASH;
-  if (ATLS_GHASH_W) f |= ATLS_BUILD_GHASH_W;
   if (!ATLS_CTR_CACHE) f |= ATLS_BUILD_NO_CTR_CACHE;
   if (ATLS_GHASH_ROT) f |= ATLS_BUILD_GHASH_ROT;
 #ifdef ATLS_TT_STAMPS

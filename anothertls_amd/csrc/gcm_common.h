@@ -103,7 +103,8 @@ __device__ __forceinline__ void ghash_mul_tab(uint32_t (&y)[4], uint32_t wb) {
 }
 
 // The same product with W lookups issued before their first use (4W VGPRs in flight): 32 / W
-// LDS round trips per multiply, where the compiler alone waits after every few lookups.
+// LDS round trips per multiply, where the compiler alone waits after every few lookups. Microbenchmarks only
+// (tools/ubench/step_ubench.hip, corun_ubench.hip): in the record kernels it failed parity at W = 16 (round 6).
 template <int W>
 __device__ __forceinline__ void ghash_mul_tab_wide(uint32_t (&y)[4], uint32_t wb) {
   uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;

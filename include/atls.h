@@ -321,7 +321,7 @@ const char* atls_device_arch(void);
 /* Compile-time experiment switches of this build (bit set, 0 for a product build). Timing
  * experiments that drop work (ATLS_DBG_*) give wrong results; tests assert this is 0. */
 enum {
-  ATLS_BUILD_DBG_SKIP = 1u, ATLS_BUILD_DBG_SHARED_GHASH = 2u, ATLS_BUILD_GHASH_W = 4u,
+  ATLS_BUILD_DBG_SKIP = 1u, ATLS_BUILD_DBG_SHARED_GHASH = 2u, ATLS_BUILD_GHASH_W = 4u /* retired, never set */,
   ATLS_BUILD_NO_CTR_CACHE = 8u, ATLS_BUILD_GHASH_ROT = 16u, ATLS_BUILD_TT_STAMPS = 32u,
   ATLS_BUILD_CLK_STAMPS = 64u
 };
