@@ -20,20 +20,21 @@ def _stale():
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force=False, verbose=False, defines=(), out=None):
-    """defines: extra -D flags (kernel tuning variants); out: alternate library path."""
+def build(force=False, verbose=False, defines=(), out=None, flags=()):
+    """defines: extra -D flags (kernel tuning variants); flags: extra compiler flags (variant builds only);
+    out: alternate library path."""
     lib = out or LIB
-    if not force and not defines and not _stale():
+    if not force and not defines and not flags and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmds, objs = [], []
     for src in SOURCES:
-        tag = "_".join(d.replace("=", "") for d in defines)
+        tag = "_".join([d.replace("=", "") for d in defines] + [str(abs(hash(flags)) % 10**8)] * bool(flags))
         obj = os.path.join(CSRC, "_obj", (tag + "_" if tag else "") + src + ".o")
         os.makedirs(os.path.dirname(obj), exist_ok=True)
         lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-result",
-               "-munsafe-fp-atomics", *[f"-D{d}" for d in defines], *lang, "-c", os.path.join(CSRC, src), "-o", obj]
+               "-munsafe-fp-atomics", *flags, *[f"-D{d}" for d in defines], *lang, "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         cmds.append(cmd)

@@ -1,4 +1,4 @@
-"""Build library variants for same-box A/Bs: python tools/build_variants.py name=DEF1,DEF2 name2= ...
+"""Build library variants for same-box A/Bs: python tools/build_variants.py name=DEF1,DEF2,+-flag name2= ...
 Each becomes anothertls_amd/variants/libatls_<name>.so (an empty define list = the default build)."""
 import importlib.util
 import os
@@ -16,7 +16,9 @@ for arg in sys.argv[1:]:
     if arg.startswith("--"):
         continue
     name, _, defs = arg.partition("=")
-    defines = tuple(d for d in defs.split(",") if d)
+    # a list item starting with '+' is a raw compiler flag ('+-mllvm +-amdgpu-sched-strategy=max-ilp')
+    defines = tuple(d for d in defs.split(",") if d and not d.startswith("+"))
+    flags = tuple(d[1:] for d in defs.split(",") if d.startswith("+"))
     out = os.path.join(vdir, f"libatls_{name}.so")
-    b.build(force=True, defines=defines or ("ATLS_VARIANT_" + name,), out=out)
-    print(out, defines)
+    b.build(force=True, defines=defines or ("ATLS_VARIANT_" + name,), out=out, flags=flags)
+    print(out, defines, flags)
